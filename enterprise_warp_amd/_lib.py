@@ -1,0 +1,90 @@
+"""ctypes binding of libewarp_hip.so (include/ewarp_hip.h).
+
+The library is built in-tree (`enterprise_warp_amd/libewarp_hip.so`, see
+csrc/Makefile / __graft_entry__.build).  There is no CPU fallback: if the
+library or a GPU is missing, the likelihood raises.
+"""
+import ctypes as C
+import os
+
+_HERE = os.path.dirname(os.path.abspath(__file__))
+LIB_PATH = os.path.join(_HERE, "libewarp_hip.so")
+
+EWH_ABI_VERSION = 1
+SPEC_POWERLAW, SPEC_TURNOVER, SPEC_FREESPEC, SPEC_CONST = 1, 2, 3, 4
+
+
+class Pref(C.Structure):
+    _fields_ = [("idx", C.c_int32), ("pad_", C.c_int32), ("cval", C.c_double)]
+
+
+class SpecEntry(C.Structure):
+    _fields_ = [("kind", C.c_int32), ("col", C.c_int32), ("p0", Pref), ("p1", Pref), ("p2", Pref),
+                ("f", C.c_double), ("df", C.c_double), ("fyr", C.c_double)]
+
+
+_dp = C.POINTER(C.c_double)
+_ip = C.POINTER(C.c_int32)
+
+
+class PulsarDesc(C.Structure):
+    _fields_ = [("n_toa", C.c_int32), ("n_col", C.c_int32), ("n_lead_const", C.c_int32), ("n_spec", C.c_int32),
+                ("basis", _dp), ("resid", _dp), ("toaerr", _dp),
+                ("n_slot", C.c_int32), ("slots", C.POINTER(Pref)),
+                ("efac_slot", _ip), ("equad_slot", _ip),
+                ("n_epoch", C.c_int32), ("epoch_start", _ip), ("epoch_stop", _ip), ("epoch_slot", _ip),
+                ("spec", C.POINTER(SpecEntry))]
+
+
+class PtaDesc(C.Structure):
+    _fields_ = [("abi_version", C.c_int32), ("n_pulsar", C.c_int32), ("n_param", C.c_int32),
+                ("white_fixed", C.c_int32), ("pulsars", C.POINTER(PulsarDesc))]
+
+
+EXPORTS = ["ewh_create", "ewh_lnl_batch", "ewh_lnl_units_device", "ewh_last_unit_terms", "ewh_unit_cost",
+           "ewh_set_kernel_mode", "ewh_destroy", "ewh_last_error", "ewh_version"]
+
+_lib = None
+
+
+class EngineError(RuntimeError):
+    pass
+
+
+def load():
+    """Load and type the shared library (does not touch the GPU)."""
+    global _lib
+    if _lib is not None:
+        return _lib
+    if not os.path.exists(LIB_PATH):
+        raise EngineError(f"{LIB_PATH} not built: run `make -C enterprise_warp_amd/csrc` or "
+                          "__graft_entry__.build(); there is no CPU fallback")
+    lib = C.CDLL(LIB_PATH)
+    lib.ewh_create.argtypes = [C.POINTER(PtaDesc), C.c_int, C.POINTER(C.c_void_p)]
+    lib.ewh_create.restype = C.c_int
+    lib.ewh_lnl_batch.argtypes = [C.c_void_p, _dp, C.c_int32, _dp]
+    lib.ewh_lnl_batch.restype = C.c_int
+    lib.ewh_lnl_units_device.argtypes = [C.c_void_p, C.c_void_p, C.c_int32, C.c_int64, C.c_int64, C.c_void_p,
+                                         C.c_void_p]
+    lib.ewh_lnl_units_device.restype = C.c_int
+    lib.ewh_last_unit_terms.argtypes = [C.c_void_p, _dp, C.c_int32]
+    lib.ewh_last_unit_terms.restype = C.c_int
+    lib.ewh_unit_cost.argtypes = [C.c_void_p, C.c_int32]
+    lib.ewh_unit_cost.restype = C.c_double
+    lib.ewh_set_kernel_mode.argtypes = [C.c_void_p, C.c_int32]
+    lib.ewh_set_kernel_mode.restype = C.c_int
+    lib.ewh_destroy.argtypes = [C.c_void_p]
+    lib.ewh_destroy.restype = None
+    lib.ewh_last_error.argtypes = []
+    lib.ewh_last_error.restype = C.c_char_p
+    lib.ewh_version.argtypes = []
+    lib.ewh_version.restype = C.c_int
+    if lib.ewh_version() != EWH_ABI_VERSION:
+        raise EngineError("libewarp_hip.so ABI version mismatch")
+    _lib = lib
+    return lib
+
+
+def check(rc):
+    if rc != 0:
+        raise EngineError(f"libewarp_hip error {rc}: {_lib.ewh_last_error().decode(errors='replace')}")

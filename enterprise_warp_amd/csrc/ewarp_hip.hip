@@ -1,0 +1,1025 @@
+// ewarp_hip.hip — MI355X (gfx950) PTA log-likelihood engine.
+//
+// Implements include/ewarp_hip.h.  The arithmetic restates the enterprise
+// likelihood that enterprise_warp drives (signal_base.PTA built at
+// enterprise_warp.py:502, called at bilby_warp.py:35):
+//
+//   lnL = sum_p [ -1/2 (r^T N^-1 r + log|N|)
+//                 + 1/2 (d^T Sigma^-1 d - log|Sigma| - log|phi|) ],
+//   Sigma = T^T N^-1 T + diag(1/phi),  d = T^T N^-1 r.
+//
+// Device formulation:
+//  * The residual vector is appended to the basis as its LAST column
+//    (T_aug = [T | pad | r]), so one contraction G = T_aug^T N^-1 T_aug gives
+//    T^T N^-1 T, d and r^T N^-1 r together, and one Cholesky of
+//    G + diag(1/phi, 0) gives, in its last pivot, q = r^T N^-1 r - d^T Sigma^-1 d.
+//    lnL_p = -1/2 log|N| - 1/2 q - sum_j log U_jj - 1/2 sum_j log phi_j.
+//  * White noise fixed: G and the elimination of the theta-independent
+//    leading (timing-model, phi = 1e40) block are computed once at create; per
+//    sample only the reduced (m - n_tm + 1)^2 factorisation runs.
+//  * Kernels: wn_weights (N, ECORR Sherman-Morrison terms), epoch_sums,
+//    contract_mfma (fp64 MFMA T^T N^-1 T with LDS-staged TOA tiles),
+//    schur (fixed-WN lead elimination), chol_mfma (one wave per
+//    (pulsar, sample): 16x16 blocks register-resident in MFMA C/D layout,
+//    panel rows by VALU + cross-lane shuffles, trailing update by
+//    v_mfma_f64_16x16x4_f64), chol_lds (general fallback, matrix in LDS),
+//    reduce_units (sum over pulsars in pulsar order).
+#include <hip/hip_runtime.h>
+
+#include <algorithm>
+#include <cmath>
+#include <cstdint>
+#include <cstring>
+#include <string>
+#include <type_traits>
+#include <vector>
+
+#include "ewarp_hip.h"
+
+namespace {
+
+thread_local std::string g_err;
+
+int set_err(int code, const std::string& msg) {
+  g_err = msg;
+  return code;
+}
+
+#define EWH_HIP(expr)                                                          \
+  do {                                                                         \
+    hipError_t e_ = (expr);                                                    \
+    if (e_ != hipSuccess)                                                      \
+      return set_err(EWH_E_HIP, std::string(#expr) + ": " + hipGetErrorString(e_)); \
+  } while (0)
+
+typedef double v4d __attribute__((ext_vector_type(4)));
+
+// ----------------------------------------------------------------------------
+// device helpers
+// ----------------------------------------------------------------------------
+__device__ __forceinline__ double pref_val(const ewh_pref& r, const double* th) {
+  return r.idx >= 0 ? th[r.idx] : r.cval;
+}
+
+// phi of one spectral entry; restates [ent] utils.powerlaw, the reference's
+// powerlaw_bpl (enterprise_models.py:553-563) and [ent] gp_priors.free_spectrum
+// with the same operation order.
+__device__ double spec_phi(const ewh_spec_entry& s, const double* th) {
+  switch (s.kind) {
+    case EWH_SPEC_POWERLAW: {
+      const double lgA = pref_val(s.p0, th), gam = pref_val(s.p1, th);
+      const double A = pow(10.0, lgA);
+      return A * A / 12.0 / (M_PI * M_PI) * pow(s.fyr, gam - 3.0) * pow(s.f, -gam) * s.df;
+    }
+    case EWH_SPEC_TURNOVER: {
+      const double lgA = pref_val(s.p0, th), gam = pref_val(s.p1, th);
+      double fc = pref_val(s.p2, th);
+      if (fc < 0) fc = pow(10.0, fc);
+      const double A = pow(10.0, lgA);
+      return A * A / 12.0 / (M_PI * M_PI) * pow(s.fyr, -3.0) * pow((s.f + fc) / s.fyr, -gam) * s.df;
+    }
+    case EWH_SPEC_FREESPEC:
+      return pow(10.0, 2.0 * pref_val(s.p0, th));
+    case EWH_SPEC_CONST:
+      return s.p0.cval;
+    default:
+      return __builtin_nan("");
+  }
+}
+
+__device__ __forceinline__ double wave_sum(double v) {
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o);
+  return v;
+}
+
+// 256-thread block sum; `scratch` holds >= 4 doubles.
+__device__ double block_sum256(double v, double* scratch) {
+  v = wave_sum(v);
+  const int w = threadIdx.x >> 6;
+  __syncthreads();
+  if ((threadIdx.x & 63) == 0) scratch[w] = v;
+  __syncthreads();
+  double t = scratch[0] + scratch[1] + scratch[2] + scratch[3];
+  __syncthreads();
+  return t;
+}
+
+// ----------------------------------------------------------------------------
+// per-pulsar device tables
+// ----------------------------------------------------------------------------
+struct PsrDev {
+  int n_toa, m, ld, nb;      // varying layout: T_aug is n_toa x ld, r at ld-1
+  int n_epoch;
+  const double* T;           // n_toa x ld row-major
+  const double* sig2;        // toaerr^2
+  const int* efac_slot;
+  const int* equad_slot;
+  const ewh_pref* slots;
+  const int* ep_start;
+  const int* ep_stop;
+  const int* ep_slot;
+};
+
+// One factorisation job: (pulsar, sample) -> matrix + diagonal update.
+struct CholJob {
+  const double* mats;        // matrix of sample b at mats + (b - b_off) * mstride
+  long long mstride;         // 0: one matrix shared by every sample
+  int ld;                    // leading dimension (= 16 * NB)
+  int mreal;                 // columns with a phi entry (0..mreal-1); r at ld-1
+  const int* col_ptr;        // CSR of spectral entries over mreal columns
+  const ewh_spec_entry* spec;
+  const double* K;           // additive constant, K[(b - b_off) * kstride]
+  int kstride;
+  int fail;                  // 1: lead block not positive definite -> -inf
+};
+
+// ----------------------------------------------------------------------------
+// white noise: w_t = 1/N_t, ECORR beta_e, -1/2 log|N|     ([ent] ShermanMorrison)
+// grid: one 256-thread block per sample of the chunk
+// ----------------------------------------------------------------------------
+__global__ __launch_bounds__(256) void wn_weights_kernel(PsrDev P, const double* __restrict__ theta,
+                                                         int ldth, int b0, double* __restrict__ w,
+                                                         double* __restrict__ beta,
+                                                         double* __restrict__ Kb) {
+  __shared__ double red[4];
+  const int bl = blockIdx.x;
+  const double* th = theta + (long long)(b0 + bl) * ldth;
+  double* wr = w + (long long)bl * P.n_toa;
+  double acc = 0.0;
+  for (int t = threadIdx.x; t < P.n_toa; t += 256) {
+    const double ef = pref_val(P.slots[P.efac_slot[t]], th);
+    double D = ef * ef * P.sig2[t];                       // MeasurementNoise
+    const int qs = P.equad_slot[t];
+    if (qs >= 0) D += pow(10.0, 2.0 * pref_val(P.slots[qs], th));  // TNEquadNoise
+    wr[t] = 1.0 / D;
+    acc += log(D);
+  }
+  __syncthreads();
+  for (int e = threadIdx.x; e < P.n_epoch; e += 256) {   // EcorrKernelNoise
+    double s = 0.0;
+    for (int t = P.ep_start[e]; t < P.ep_stop[e]; ++t) s += wr[t];
+    const double J = pow(10.0, 2.0 * pref_val(P.slots[P.ep_slot[e]], th));
+    const double be = 1.0 / (s + 1.0 / J);
+    beta[(long long)bl * P.n_epoch + e] = be;
+    acc += log(J) - log(be);
+  }
+  acc = block_sum256(acc, red);
+  if (threadIdx.x == 0) Kb[bl] = -0.5 * acc;
+}
+
+// s[bl][e][:] = sum_{t in epoch e} w_t T_aug[t][:]
+__global__ __launch_bounds__(256) void epoch_sums_kernel(PsrDev P, const double* __restrict__ w,
+                                                         double* __restrict__ s) {
+  const int e = blockIdx.x, bl = blockIdx.y;
+  const double* wr = w + (long long)bl * P.n_toa;
+  double* out = s + ((long long)bl * P.n_epoch + e) * P.ld;
+  const int t0 = P.ep_start[e], t1 = P.ep_stop[e];
+  for (int c = threadIdx.x; c < P.ld; c += 256) {
+    double a = 0.0;
+    for (int t = t0; t < t1; ++t) a += wr[t] * P.T[(long long)t * P.ld + c];
+    out[c] = a;
+  }
+}
+
+// ----------------------------------------------------------------------------
+// fp64 MFMA contraction G = T_aug^T W T_aug - sum_e beta_e s_e s_e^T
+// One 256-thread workgroup (4 waves) per sample; the NB(NB+1)/2 upper 16x16
+// output blocks are dealt round-robin to the waves; 32-row TOA tiles are
+// staged in LDS and shared by the four waves.
+// ----------------------------------------------------------------------------
+constexpr int CT_ROWS = 32;
+
+template <int NB>
+__global__ __launch_bounds__(256) void contract_mfma_kernel(PsrDev P, const double* __restrict__ w,
+                                                            const double* __restrict__ beta,
+                                                            const double* __restrict__ s,
+                                                            double* __restrict__ G) {
+  constexpr int LD = 16 * NB;
+  constexpr int NBLK = NB * (NB + 1) / 2;
+  constexpr int SLOTS = (NBLK + 3) / 4;
+  extern __shared__ __attribute__((aligned(16))) double smem[];
+  double* tile = smem;                     // CT_ROWS x LD
+  double* wt = smem + CT_ROWS * LD;        // CT_ROWS weights
+  const int bl = blockIdx.x;
+  const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63, q = lane >> 4, c = lane & 15;
+
+  int bi[SLOTS], bj[SLOTS];
+  bool valid[SLOTS];
+#pragma unroll
+  for (int sl = 0; sl < SLOTS; ++sl) {
+    int blk = wave + 4 * sl;
+    valid[sl] = blk < NBLK;
+    int i = 0;
+    while (blk >= NB - i && i < NB - 1) { blk -= NB - i; ++i; }
+    bi[sl] = i;
+    bj[sl] = i + blk;
+  }
+  v4d acc[SLOTS];
+#pragma unroll
+  for (int sl = 0; sl < SLOTS; ++sl) acc[sl] = v4d{0.0, 0.0, 0.0, 0.0};
+
+  // pass 0: TOA rows (weights w), pass 1: epoch rows (weights -beta)
+  for (int pass = 0; pass < 2; ++pass) {
+    const int nrows = pass == 0 ? P.n_toa : P.n_epoch;
+    const double* src = pass == 0 ? P.T : s + (long long)bl * P.n_epoch * LD;
+    const double* wsrc = pass == 0 ? w + (long long)bl * P.n_toa : beta + (long long)bl * P.n_epoch;
+    const double wsign = pass == 0 ? 1.0 : -1.0;
+    for (int t0 = 0; t0 < nrows; t0 += CT_ROWS) {
+      const int rows = min(CT_ROWS, nrows - t0);
+      for (int idx = threadIdx.x; idx < CT_ROWS * LD; idx += 256)
+        tile[idx] = idx < rows * LD ? src[(long long)t0 * LD + idx] : 0.0;
+      if (threadIdx.x < CT_ROWS) wt[threadIdx.x] = threadIdx.x < rows ? wsign * wsrc[t0 + threadIdx.x] : 0.0;
+      __syncthreads();
+#pragma unroll
+      for (int kk = 0; kk < CT_ROWS / 4; ++kk) {
+        const int row = 4 * kk + q;
+        const double wr = wt[row];
+        const double* trow = tile + row * LD + c;
+#pragma unroll
+        for (int sl = 0; sl < SLOTS; ++sl) {
+          if (valid[sl]) {
+            const double a = wr * trow[16 * bi[sl]];
+            const double b = trow[16 * bj[sl]];
+            acc[sl] = __builtin_amdgcn_mfma_f64_16x16x4f64(a, b, acc[sl], 0, 0, 0);
+          }
+        }
+      }
+      __syncthreads();
+    }
+  }
+  // epilogue: C/D layout lane -> (row q + 4r, col c); mirror to the lower half,
+  // unit diagonal on pad columns (m .. LD-2) so they factor as identity.
+  double* out = G + (long long)bl * LD * LD;
+#pragma unroll
+  for (int sl = 0; sl < SLOTS; ++sl) {
+    if (!valid[sl]) continue;
+#pragma unroll
+    for (int r = 0; r < 4; ++r) {
+      const int row = 16 * bi[sl] + q + 4 * r, col = 16 * bj[sl] + c;
+      double v = acc[sl][r];
+      if (row == col && row >= P.m && row < LD - 1) v = 1.0;
+      out[(long long)row * LD + col] = v;
+      out[(long long)col * LD + row] = v;
+    }
+  }
+}
+
+// ----------------------------------------------------------------------------
+// fixed white noise: eliminate the leading constant-phi (timing-model) block
+// of G once; write the reduced matrix S (fx_ld x fx_ld, r last) and K.
+// One 256-thread block per pulsar; G is modified in place.
+// ----------------------------------------------------------------------------
+__global__ __launch_bounds__(256) void schur_kernel(double* G, int ld, int m, int nlead,
+                                                    const int* __restrict__ col_ptr,
+                                                    const ewh_spec_entry* __restrict__ spec,
+                                                    double Kb, double* S, int fx_ld, int fx_m,
+                                                    double* Kout, int* fail_out) {
+  __shared__ double row[256 * 4];
+  __shared__ double red[4];
+  double lphi = 0.0;
+  for (int a = threadIdx.x; a < nlead; a += 256) {
+    double ph = 0.0;
+    for (int e = col_ptr[a]; e < col_ptr[a + 1]; ++e) ph += spec_phi(spec[e], nullptr);
+    G[(long long)a * ld + a] += 1.0 / ph;
+    lphi += log(ph);
+  }
+  lphi = block_sum256(lphi, red);
+  __syncthreads();
+  double logdet = 0.0;
+  int ok = 1;
+  for (int k = 0; k < nlead; ++k) {
+    const double piv = G[(long long)k * ld + k];
+    ok &= piv > 0.0;
+    const double d = sqrt(piv), rinv = 1.0 / d;
+    logdet += log(d);
+    __syncthreads();
+    for (int j = k + 1 + threadIdx.x; j < ld; j += 256) row[j] = G[(long long)k * ld + j] * rinv;
+    __syncthreads();
+    for (int i = k + 1; i < ld; ++i) {
+      const double ri = row[i];
+      for (int j = k + 1 + threadIdx.x; j < ld; j += 256) G[(long long)i * ld + j] -= ri * row[j];
+    }
+    __syncthreads();
+  }
+  // reduced index a -> G column: a < fx_m -> nlead + a ; a == fx_ld-1 -> ld-1 ; else pad
+  for (int idx = threadIdx.x; idx < fx_ld * fx_ld; idx += 256) {
+    const int a = idx / fx_ld, bcol = idx % fx_ld;
+    const int ga = a < fx_m ? nlead + a : (a == fx_ld - 1 ? ld - 1 : -1);
+    const int gb = bcol < fx_m ? nlead + bcol : (bcol == fx_ld - 1 ? ld - 1 : -1);
+    double v;
+    if (ga < 0 || gb < 0) v = (a == bcol) ? 1.0 : 0.0;
+    else v = G[(long long)ga * ld + gb];
+    S[idx] = v;
+  }
+  if (threadIdx.x == 0) {
+    *Kout = Kb - logdet - 0.5 * lphi;
+    *fail_out = ok ? 0 : 1;
+  }
+}
+
+// ----------------------------------------------------------------------------
+// batched Cholesky, general fallback: one 256-thread block per unit, the
+// (compacted) matrix as a packed lower triangle in LDS.
+// ----------------------------------------------------------------------------
+__global__ __launch_bounds__(256) void chol_lds_kernel(const CholJob* __restrict__ jobs, int B,
+                                                       long long u0, int b_off,
+                                                       const double* __restrict__ theta, int ldth,
+                                                       double* __restrict__ out_units) {
+  extern __shared__ __attribute__((aligned(16))) double sm[];
+  __shared__ double red[4];
+  const long long u = u0 + blockIdx.x;
+  const int p = (int)(u / B), b = (int)(u % B);
+  const CholJob J = jobs[p];
+  const int mr = J.mreal, ma = mr + 1, ld = J.ld;
+  double* L = sm;                               // ma(ma+1)/2
+  double* col = sm + (long long)ma * (ma + 1) / 2;
+  const double* A = J.mats + (long long)(b - b_off) * J.mstride;
+  const double* th = theta + (long long)b * ldth;
+  const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
+  for (int i = wave; i < ma; i += 4) {
+    const int gi = i < mr ? i : ld - 1;
+    const int base = i * (i + 1) / 2;
+    for (int j = lane; j <= i; j += 64) L[base + j] = A[(long long)gi * ld + (j < mr ? j : ld - 1)];
+  }
+  __syncthreads();
+  double lphi = 0.0;
+  for (int a = threadIdx.x; a < mr; a += 256) {
+    double ph = 0.0;
+    for (int e = J.col_ptr[a]; e < J.col_ptr[a + 1]; ++e) ph += spec_phi(J.spec[e], th);
+    L[a * (a + 1) / 2 + a] += 1.0 / ph;
+    lphi += log(ph);
+  }
+  lphi = block_sum256(lphi, red);
+  __syncthreads();
+  double logdet = 0.0;
+  bool ok = true;
+  for (int k = 0; k < ma - 1; ++k) {
+    const double piv = L[k * (k + 1) / 2 + k];
+    ok = ok && (piv > 0.0);
+    const double d = sqrt(piv), rinv = 1.0 / d;
+    logdet += log(d);
+    for (int i = k + 1 + threadIdx.x; i < ma; i += 256) col[i] = L[i * (i + 1) / 2 + k] * rinv;
+    __syncthreads();
+    for (int i = k + 1 + wave; i < ma; i += 4) {
+      const double ci = col[i];
+      const int base = i * (i + 1) / 2;
+      for (int j = k + 1 + lane; j <= i; j += 64) L[base + j] -= ci * col[j];
+    }
+    __syncthreads();
+  }
+  const double qv = L[(ma - 1) * ma / 2 + ma - 1];
+  if (threadIdx.x == 0) {
+    double lnl = J.K[(long long)(b - b_off) * J.kstride] - 0.5 * qv - logdet - 0.5 * lphi;
+    if (!ok || J.fail) lnl = -INFINITY;
+    out_units[(long long)p * B + b] = lnl;
+  }
+}
+
+// ----------------------------------------------------------------------------
+// batched Cholesky, MFMA register-blocked: one wave (64 lanes) per unit.
+// The upper triangle of the LD x LD matrix (LD = 16 NB) lives in registers as
+// NB(NB+1)/2 16x16 blocks in the v_mfma_f64_16x16x4_f64 C/D layout
+// (lane l, reg r <-> row (l>>4) + 4r, col l&15).  Factor A = U^T U (upper,
+// as LAPACK dpotrf 'U' behind scipy cho_factor): for each block row b the
+// 16 pivots of the panel are done by VALU with cross-lane shuffles, then the
+// trailing blocks get A_ij -= U_bi^T U_bj by four MFMAs each — U_bi's
+// register s IS the MFMA A operand of k-slice s and U_bj's the B operand,
+// so the update needs no data movement at all.
+// ----------------------------------------------------------------------------
+template <int NB>
+struct Tri {
+  static constexpr int n = NB * (NB + 1) / 2;
+  static constexpr int idx(int i, int j) { return i * NB - (i * (i - 1)) / 2 + (j - i); }
+};
+
+// compile-time loop: f(std::integral_constant<int, I>) for I in [B, E)
+template <int B, int E, typename F>
+__device__ __forceinline__ void static_for(F&& f) {
+  if constexpr (B < E) {
+    f(std::integral_constant<int, B>{});
+    static_for<B + 1, E>(f);
+  }
+}
+
+template <int NB>
+__global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(1, 1)))
+void chol_mfma_kernel(const CholJob* __restrict__ jobs, int B, long long u0, int b_off,
+                      const double* __restrict__ theta, int ldth, double* __restrict__ out_units) {
+  constexpr int LD = 16 * NB;
+  using T = Tri<NB>;
+  __shared__ double phinv[LD];
+  const int lane = threadIdx.x;
+  const int q = lane >> 4, c = lane & 15;
+  const long long u = u0 + blockIdx.x;
+  const int p = (int)(u / B), b = (int)(u % B);
+  const CholJob J = jobs[p];
+  const double* A = J.mats + (long long)(b - b_off) * J.mstride;
+  const double* th = theta + (long long)b * ldth;
+
+  double lphi = 0.0;
+  for (int a = lane; a < LD; a += 64) {
+    double pi = 0.0;
+    if (a < J.mreal) {
+      double ph = 0.0;
+      for (int e = J.col_ptr[a]; e < J.col_ptr[a + 1]; ++e) ph += spec_phi(J.spec[e], th);
+      pi = 1.0 / ph;
+      lphi += log(ph);
+    }
+    phinv[a] = pi;
+  }
+  lphi = wave_sum(lphi);
+  __syncthreads();
+
+  v4d U[T::n];
+  static_for<0, NB>([&](auto BI) {
+    constexpr int bi = decltype(BI)::value;
+    static_for<bi, NB>([&](auto BJ) {
+      constexpr int bj = decltype(BJ)::value;
+      v4d v;
+      static_for<0, 4>([&](auto R) {
+        constexpr int r = decltype(R)::value;
+        v[r] = A[(long long)(16 * bi + q + 4 * r) * LD + 16 * bj + c];
+      });
+      if constexpr (bi == bj) {
+        const double pd = phinv[16 * bi + c];
+        static_for<0, 4>([&](auto R) {
+          constexpr int r = decltype(R)::value;
+          v[r] += (q + 4 * r == c) ? pd : 0.0;
+        });
+      }
+      U[T::idx(bi, bj)] = v;
+    });
+  });
+
+  double logdet = 0.0;
+  bool ok = true;
+  static_for<0, NB>([&](auto BB) {
+    constexpr int bb = decltype(BB)::value;
+    // panel row bb: 16 pivots by VALU (the r column, last of all, is not pivoted)
+    static_for<0, (bb == NB - 1 ? 15 : 16)>([&](auto K) {
+      constexpr int k = decltype(K)::value;
+      constexpr int kq = k & 3, kr = k >> 2;
+      const double piv = __shfl(U[T::idx(bb, bb)][kr], 16 * kq + k);
+      ok = ok && (piv > 0.0);
+      const double d = sqrt(piv), rinv = 1.0 / d;
+      logdet += log(d);
+      const bool rowk = (q == kq);
+      double rk[NB];
+      static_for<bb, NB>([&](auto JJ) {
+        constexpr int j = decltype(JJ)::value;
+        double x = U[T::idx(bb, j)][kr];
+        x = rowk ? x * rinv : x;
+        U[T::idx(bb, j)][kr] = x;
+        rk[j] = __shfl(x, 16 * kq + c);               // U[k][col c] of block (bb, j)
+      });
+      double ui[4];
+      static_for<0, 4>([&](auto R) {
+        constexpr int r = decltype(R)::value;
+        const double v = __shfl(U[T::idx(bb, bb)][kr], 16 * kq + q + 4 * r);  // U[k][q+4r]
+        ui[r] = (q + 4 * r > k) ? v : 0.0;
+      });
+      static_for<bb, NB>([&](auto JJ) {
+        constexpr int j = decltype(JJ)::value;
+        static_for<0, 4>([&](auto R) {
+          constexpr int r = decltype(R)::value;
+          U[T::idx(bb, j)][r] = fma(-ui[r], rk[j], U[T::idx(bb, j)][r]);
+        });
+      });
+    });
+    // trailing update A_ij -= U_bi^T U_bj, four f64 MFMAs per block
+    static_for<bb + 1, NB>([&](auto II) {
+      constexpr int i = decltype(II)::value;
+      static_for<i, NB>([&](auto JJ) {
+        constexpr int j = decltype(JJ)::value;
+        static_for<0, 4>([&](auto S) {
+          constexpr int sk = decltype(S)::value;
+          U[T::idx(i, j)] = __builtin_amdgcn_mfma_f64_16x16x4f64(-U[T::idx(bb, i)][sk], U[T::idx(bb, j)][sk],
+                                                                 U[T::idx(i, j)], 0, 0, 0);
+        });
+      });
+    });
+  });
+  const double qv = __shfl(U[T::idx(NB - 1, NB - 1)][3], 63);
+  if (lane == 0) {
+    double lnl = J.K[(long long)(b - b_off) * J.kstride] - 0.5 * qv - logdet - 0.5 * lphi;
+    if (!ok || J.fail) lnl = -INFINITY;
+    out_units[(long long)p * B + b] = lnl;
+  }
+}
+
+// out[b] = sum_p units[p * B + b], pulsars in order.
+__global__ void reduce_units_kernel(const double* __restrict__ units, int P, int B, double* __restrict__ out) {
+  const int b = blockIdx.x * blockDim.x + threadIdx.x;
+  if (b >= B) return;
+  double s = 0.0;
+  for (int p = 0; p < P; ++p) s += units[(long long)p * B + b];
+  out[b] = s;
+}
+
+// ----------------------------------------------------------------------------
+// host side
+// ----------------------------------------------------------------------------
+constexpr int MFMA_NB_MAX = 9;
+constexpr size_t LDS_MAX = 160 * 1024;
+
+struct PsrHost {
+  int n_toa = 0, m = 0, nlead = 0, ld = 0, nb = 0, n_epoch = 0;
+  int fx_m = 0, fx_ld = 0, fx_nb = 0;
+  PsrDev dev{};
+  int* d_colptr = nullptr;        // varying CSR (m+1)
+  ewh_spec_entry* d_spec = nullptr;
+  int* d_fx_colptr = nullptr;     // fixed CSR (fx_m+1), entries re-indexed
+  ewh_spec_entry* d_fx_spec = nullptr;
+  double* d_S = nullptr;          // fx_ld^2
+  bool has_theta_white = false;
+};
+
+}  // namespace
+
+struct ewh_handle {
+  int device = 0;
+  int P = 0, n_param = 0;
+  bool white_fixed = false;
+  int kernel_mode = 0;
+  hipStream_t stream = nullptr;
+  std::vector<PsrHost> psr;
+  std::vector<void*> allocs;
+  CholJob* d_jobs_fixed = nullptr;
+  CholJob* d_jobs_var = nullptr;
+  double* d_fxK = nullptr;
+  int* d_fxfail = nullptr;
+  // per-call scratch
+  double* d_units = nullptr;
+  size_t units_cap = 0;
+  double* d_theta = nullptr;
+  double* d_out = nullptr;
+  size_t io_cap = 0;
+  // varying-WN scratch
+  double *d_w = nullptr, *d_beta = nullptr, *d_s = nullptr, *d_G = nullptr, *d_Kb = nullptr;
+  int chunk = 0;
+  int last_B = 0;
+};
+
+namespace {
+
+template <typename T>
+int dalloc(ewh_handle* h, T** p, size_t count) {
+  *p = nullptr;
+  if (count == 0) count = 1;
+  hipError_t e = hipMalloc((void**)p, count * sizeof(T));
+  if (e != hipSuccess) return set_err(EWH_E_NOMEM, std::string("hipMalloc: ") + hipGetErrorString(e));
+  h->allocs.push_back(*p);
+  return 0;
+}
+
+template <typename T>
+int dupload(ewh_handle* h, T** p, const T* src, size_t count) {
+  int rc = dalloc(h, p, count);
+  if (rc) return rc;
+  if (count) EWH_HIP(hipMemcpy(*p, src, count * sizeof(T), hipMemcpyHostToDevice));
+  return 0;
+}
+
+int nb_for(int cols_with_r) { return (cols_with_r + 15) / 16; }
+
+size_t lds_bytes_chol(int mreal) {
+  const size_t ma = (size_t)mreal + 1;
+  return (ma * (ma + 1) / 2 + ma) * sizeof(double);
+}
+
+bool pref_uses_theta(const ewh_pref& r) { return r.idx >= 0; }
+
+int validate(const ewh_pta_desc* d) {
+  if (!d || d->abi_version != EWH_ABI_VERSION) return set_err(EWH_E_INVALID, "bad descriptor / ABI version");
+  if (d->n_pulsar <= 0 || !d->pulsars) return set_err(EWH_E_INVALID, "no pulsars");
+  if (d->n_param < 0) return set_err(EWH_E_INVALID, "n_param < 0");
+  for (int p = 0; p < d->n_pulsar; ++p) {
+    const ewh_pulsar_desc& s = d->pulsars[p];
+    const std::string tag = "pulsar " + std::to_string(p) + ": ";
+    if (s.n_toa <= 0 || s.n_col < 0 || s.n_lead_const < 0 || s.n_lead_const > s.n_col)
+      return set_err(EWH_E_INVALID, tag + "bad sizes");
+    if ((s.n_col && !s.basis) || !s.resid || !s.toaerr || !s.efac_slot || !s.equad_slot ||
+        (s.n_slot && !s.slots) || (s.n_spec && !s.spec))
+      return set_err(EWH_E_INVALID, tag + "null pointer");
+    if (s.n_epoch && (!s.epoch_start || !s.epoch_stop || !s.epoch_slot))
+      return set_err(EWH_E_INVALID, tag + "null epoch pointer");
+    for (int i = 0; i < s.n_slot; ++i)
+      if (s.slots[i].idx >= d->n_param) return set_err(EWH_E_INVALID, tag + "slot theta index out of range");
+    for (int t = 0; t < s.n_toa; ++t) {
+      if (s.efac_slot[t] < 0 || s.efac_slot[t] >= s.n_slot) return set_err(EWH_E_INVALID, tag + "efac slot out of range");
+      if (s.equad_slot[t] >= s.n_slot) return set_err(EWH_E_INVALID, tag + "equad slot out of range");
+    }
+    int prev = 0;
+    for (int e = 0; e < s.n_epoch; ++e) {
+      if (s.epoch_start[e] < prev || s.epoch_stop[e] <= s.epoch_start[e] + 1 || s.epoch_stop[e] > s.n_toa)
+        return set_err(EWH_E_INVALID, tag + "epochs must be ordered, disjoint slices of >= 2 TOAs");
+      if (s.epoch_slot[e] < 0 || s.epoch_slot[e] >= s.n_slot) return set_err(EWH_E_INVALID, tag + "epoch slot out of range");
+      prev = s.epoch_stop[e];
+    }
+    std::vector<int> cnt(s.n_col, 0);
+    for (int e = 0; e < s.n_spec; ++e) {
+      const ewh_spec_entry& sp = s.spec[e];
+      if (sp.col < 0 || sp.col >= s.n_col) return set_err(EWH_E_INVALID, tag + "spectral column out of range");
+      if (sp.kind < EWH_SPEC_POWERLAW || sp.kind > EWH_SPEC_CONST) return set_err(EWH_E_INVALID, tag + "bad spectral kind");
+      if (sp.p0.idx >= d->n_param || sp.p1.idx >= d->n_param || sp.p2.idx >= d->n_param)
+        return set_err(EWH_E_INVALID, tag + "spectral theta index out of range");
+      if (sp.col < s.n_lead_const && sp.kind != EWH_SPEC_CONST)
+        return set_err(EWH_E_INVALID, tag + "leading columns must have constant phi");
+      cnt[sp.col]++;
+    }
+    for (int j = 0; j < s.n_col; ++j)
+      if (!cnt[j]) return set_err(EWH_E_INVALID, tag + "column " + std::to_string(j) + " has no phi entry");
+  }
+  return 0;
+}
+
+// CSR over columns [c0, c1) re-indexed to start at 0.
+void build_csr(const ewh_pulsar_desc& s, int c0, int c1, std::vector<int>& ptr, std::vector<ewh_spec_entry>& ent) {
+  const int n = c1 - c0;
+  ptr.assign(n + 1, 0);
+  for (int e = 0; e < s.n_spec; ++e)
+    if (s.spec[e].col >= c0 && s.spec[e].col < c1) ptr[s.spec[e].col - c0 + 1]++;
+  for (int j = 0; j < n; ++j) ptr[j + 1] += ptr[j];
+  ent.assign(ptr[n], ewh_spec_entry{});
+  std::vector<int> fill(ptr.begin(), ptr.end() - 1);
+  for (int e = 0; e < s.n_spec; ++e) {  // keeps the caller's entry order per column
+    const int cc = s.spec[e].col;
+    if (cc >= c0 && cc < c1) {
+      ewh_spec_entry x = s.spec[e];
+      x.col = cc - c0;
+      ent[fill[cc - c0]++] = x;
+    }
+  }
+}
+
+template <int NB>
+void launch_contract(const PsrDev& P, const double* w, const double* beta, const double* s, double* G, int nb_samples,
+                     hipStream_t st) {
+  const size_t lds = (size_t)(CT_ROWS * 16 * NB + CT_ROWS) * sizeof(double);
+  hipLaunchKernelGGL(HIP_KERNEL_NAME(contract_mfma_kernel<NB>), dim3(nb_samples), dim3(256), lds, st, P, w, beta, s, G);
+}
+
+int dispatch_contract(int nb, const PsrDev& P, const double* w, const double* beta, const double* s, double* G,
+                      int nb_samples, hipStream_t st) {
+  switch (nb) {
+    case 1: launch_contract<1>(P, w, beta, s, G, nb_samples, st); break;
+    case 2: launch_contract<2>(P, w, beta, s, G, nb_samples, st); break;
+    case 3: launch_contract<3>(P, w, beta, s, G, nb_samples, st); break;
+    case 4: launch_contract<4>(P, w, beta, s, G, nb_samples, st); break;
+    case 5: launch_contract<5>(P, w, beta, s, G, nb_samples, st); break;
+    case 6: launch_contract<6>(P, w, beta, s, G, nb_samples, st); break;
+    case 7: launch_contract<7>(P, w, beta, s, G, nb_samples, st); break;
+    case 8: launch_contract<8>(P, w, beta, s, G, nb_samples, st); break;
+    case 9: launch_contract<9>(P, w, beta, s, G, nb_samples, st); break;
+    case 10: launch_contract<10>(P, w, beta, s, G, nb_samples, st); break;
+    case 11: launch_contract<11>(P, w, beta, s, G, nb_samples, st); break;
+    case 12: launch_contract<12>(P, w, beta, s, G, nb_samples, st); break;
+    case 13: launch_contract<13>(P, w, beta, s, G, nb_samples, st); break;
+    default: return set_err(EWH_E_UNSUPPORTED, "basis too wide for the contraction kernel (> 207 columns)");
+  }
+  return 0;
+}
+
+template <int NB>
+void launch_chol_mfma(const CholJob* jobs, int B, long long u0, long long n, int b_off, const double* theta, int ldth,
+                      double* units, hipStream_t st) {
+  hipLaunchKernelGGL(HIP_KERNEL_NAME(chol_mfma_kernel<NB>), dim3((unsigned)n), dim3(64), 0, st, jobs, B, u0, b_off,
+                     theta, ldth, units);
+}
+
+int dispatch_chol(int mode, int nb, int mreal, const CholJob* jobs, int B, long long u0, long long n, int b_off,
+                  const double* theta, int ldth, double* units, hipStream_t st) {
+  if (n <= 0) return 0;
+  if (mode == 0 && nb <= MFMA_NB_MAX) {
+    switch (nb) {
+      case 1: launch_chol_mfma<1>(jobs, B, u0, n, b_off, theta, ldth, units, st); return 0;
+      case 2: launch_chol_mfma<2>(jobs, B, u0, n, b_off, theta, ldth, units, st); return 0;
+      case 3: launch_chol_mfma<3>(jobs, B, u0, n, b_off, theta, ldth, units, st); return 0;
+      case 4: launch_chol_mfma<4>(jobs, B, u0, n, b_off, theta, ldth, units, st); return 0;
+      case 5: launch_chol_mfma<5>(jobs, B, u0, n, b_off, theta, ldth, units, st); return 0;
+      case 6: launch_chol_mfma<6>(jobs, B, u0, n, b_off, theta, ldth, units, st); return 0;
+      case 7: launch_chol_mfma<7>(jobs, B, u0, n, b_off, theta, ldth, units, st); return 0;
+      case 8: launch_chol_mfma<8>(jobs, B, u0, n, b_off, theta, ldth, units, st); return 0;
+      case 9: launch_chol_mfma<9>(jobs, B, u0, n, b_off, theta, ldth, units, st); return 0;
+      default: break;
+    }
+  }
+  const size_t lds = lds_bytes_chol(mreal);
+  if (lds > LDS_MAX - 64) return set_err(EWH_E_UNSUPPORTED, "reduced matrix too large for the LDS Cholesky kernel");
+  static bool attr_set = false;
+  if (!attr_set) {
+    EWH_HIP(hipFuncSetAttribute((const void*)chol_lds_kernel, hipFuncAttributeMaxDynamicSharedMemorySize,
+                                (int)(LDS_MAX - 64)));
+    attr_set = true;
+  }
+  hipLaunchKernelGGL(chol_lds_kernel, dim3((unsigned)n), dim3(256), lds, st, jobs, B, u0, b_off, theta, ldth, units);
+  return 0;
+}
+
+int ensure_units(ewh_handle* h, int B) {
+  const size_t need = (size_t)h->P * B;
+  if (need <= h->units_cap) return 0;
+  if (h->d_units) {
+    hipFree(h->d_units);
+    h->allocs.erase(std::find(h->allocs.begin(), h->allocs.end(), (void*)h->d_units));
+  }
+  h->units_cap = 0;
+  int rc = dalloc(h, &h->d_units, need);
+  if (rc) return rc;
+  h->units_cap = need;
+  return 0;
+}
+
+int ensure_var_scratch(ewh_handle* h, int B) {
+  if (h->white_fixed) return 0;
+  if (h->chunk > 0 && (h->chunk >= B || h->chunk >= 1024)) return 0;
+  for (void* p : {(void*)h->d_w, (void*)h->d_beta, (void*)h->d_s, (void*)h->d_G, (void*)h->d_Kb}) {
+    if (p) {
+      hipFree(p);
+      h->allocs.erase(std::find(h->allocs.begin(), h->allocs.end(), p));
+    }
+  }
+  size_t maxn = 1, maxe = 1, maxld = 16;
+  for (auto& ps : h->psr) {
+    maxn = std::max(maxn, (size_t)ps.n_toa);
+    maxe = std::max(maxe, (size_t)ps.n_epoch);
+    maxld = std::max(maxld, (size_t)ps.ld);
+  }
+  // chunk: keep G (ld^2) and s (E*ld) scratch under ~1.5 GB
+  const size_t per = (maxld * maxld + maxe * maxld + maxn + maxe + 1) * sizeof(double);
+  size_t chunk = std::max<size_t>(1, (size_t)1536 * 1024 * 1024 / per);
+  chunk = std::min<size_t>(chunk, std::min<size_t>(std::max(B, 1), 1024));
+  int rc;
+  if ((rc = dalloc(h, &h->d_w, chunk * maxn))) return rc;
+  if ((rc = dalloc(h, &h->d_beta, chunk * maxe))) return rc;
+  if ((rc = dalloc(h, &h->d_s, chunk * maxe * maxld))) return rc;
+  if ((rc = dalloc(h, &h->d_G, chunk * maxld * maxld))) return rc;
+  if ((rc = dalloc(h, &h->d_Kb, chunk))) return rc;
+  h->chunk = (int)chunk;
+  std::vector<CholJob> jobs(h->P);
+  for (int p = 0; p < h->P; ++p) {
+    const PsrHost& ps = h->psr[p];
+    jobs[p] = CholJob{h->d_G, (long long)ps.ld * ps.ld, ps.ld, ps.m, ps.d_colptr, ps.d_spec, h->d_Kb, 1, 0};
+  }
+  EWH_HIP(hipMemcpy(h->d_jobs_var, jobs.data(), sizeof(CholJob) * h->P, hipMemcpyHostToDevice));
+  return 0;
+}
+
+// white-noise terms of one pulsar for samples [b0, b0 + nb) into the chunk scratch
+int run_white(ewh_handle* h, int p, const double* theta, int ldth, int b0, int nb) {
+  PsrHost& ps = h->psr[p];
+  hipLaunchKernelGGL(wn_weights_kernel, dim3(nb), dim3(256), 0, h->stream, ps.dev, theta, ldth, b0, h->d_w,
+                     h->d_beta, h->d_Kb);
+  if (ps.n_epoch > 0)
+    hipLaunchKernelGGL(epoch_sums_kernel, dim3(ps.n_epoch, nb), dim3(256), 0, h->stream, ps.dev, h->d_w, h->d_s);
+  int rc = dispatch_contract(ps.nb, ps.dev, h->d_w, h->d_beta, h->d_s, h->d_G, nb, h->stream);
+  if (rc) return rc;
+  EWH_HIP(hipGetLastError());
+  return 0;
+}
+
+int setup_fixed(ewh_handle* h, const ewh_pta_desc* d) {
+  // one-sample scratch; theta is never read (all white-noise slots constant)
+  int rc;
+  size_t maxn = 1, maxe = 1, maxld = 16;
+  for (auto& ps : h->psr) {
+    maxn = std::max(maxn, (size_t)ps.n_toa);
+    maxe = std::max(maxe, (size_t)ps.n_epoch);
+    maxld = std::max(maxld, (size_t)ps.ld);
+  }
+  double *w, *beta, *s, *G, *Kb;
+  if ((rc = dalloc(h, &w, maxn))) return rc;
+  if ((rc = dalloc(h, &beta, maxe))) return rc;
+  if ((rc = dalloc(h, &s, maxe * maxld))) return rc;
+  if ((rc = dalloc(h, &G, maxld * maxld))) return rc;
+  if ((rc = dalloc(h, &Kb, 1))) return rc;
+  double* dummy_theta;
+  if ((rc = dalloc(h, &dummy_theta, std::max(1, d->n_param)))) return rc;
+  EWH_HIP(hipMemset(dummy_theta, 0, sizeof(double) * std::max(1, d->n_param)));
+  if ((rc = dalloc(h, &h->d_fxK, h->P))) return rc;
+  if ((rc = dalloc(h, &h->d_fxfail, h->P))) return rc;
+  std::vector<CholJob> jobs(h->P);
+  for (int p = 0; p < h->P; ++p) {
+    PsrHost& ps = h->psr[p];
+    hipLaunchKernelGGL(wn_weights_kernel, dim3(1), dim3(256), 0, h->stream, ps.dev, dummy_theta, 0, 0, w, beta, Kb);
+    if (ps.n_epoch > 0)
+      hipLaunchKernelGGL(epoch_sums_kernel, dim3(ps.n_epoch, 1), dim3(256), 0, h->stream, ps.dev, w, s);
+    if ((rc = dispatch_contract(ps.nb, ps.dev, w, beta, s, G, 1, h->stream))) return rc;
+    double Kb_h = 0.0;
+    EWH_HIP(hipMemcpyAsync(&Kb_h, Kb, sizeof(double), hipMemcpyDeviceToHost, h->stream));
+    EWH_HIP(hipStreamSynchronize(h->stream));
+    if ((rc = dalloc(h, &ps.d_S, (size_t)ps.fx_ld * ps.fx_ld))) return rc;
+    hipLaunchKernelGGL(schur_kernel, dim3(1), dim3(256), 0, h->stream, G, ps.ld, ps.m, ps.nlead, ps.d_colptr,
+                       ps.d_spec, Kb_h, ps.d_S, ps.fx_ld, ps.fx_m, h->d_fxK + p, h->d_fxfail + p);
+    EWH_HIP(hipGetLastError());
+    EWH_HIP(hipStreamSynchronize(h->stream));
+    int fail = 0;
+    EWH_HIP(hipMemcpy(&fail, h->d_fxfail + p, sizeof(int), hipMemcpyDeviceToHost));
+    jobs[p] = CholJob{ps.d_S, 0, ps.fx_ld, ps.fx_m, ps.d_fx_colptr, ps.d_fx_spec, h->d_fxK + p, 0, fail};
+  }
+  EWH_HIP(hipMemcpy(h->d_jobs_fixed, jobs.data(), sizeof(CholJob) * h->P, hipMemcpyHostToDevice));
+  return 0;
+}
+
+}  // namespace
+
+extern "C" {
+
+int ewh_version(void) { return EWH_ABI_VERSION; }
+
+const char* ewh_last_error(void) { return g_err.c_str(); }
+
+int ewh_create(const ewh_pta_desc* d, int device, ewh_handle** out) {
+  if (!out) return set_err(EWH_E_INVALID, "out is NULL");
+  *out = nullptr;
+  int rc = validate(d);
+  if (rc) return rc;
+  EWH_HIP(hipSetDevice(device));
+  ewh_handle* h = new ewh_handle();
+  h->device = device;
+  h->P = d->n_pulsar;
+  h->n_param = d->n_param;
+  h->psr.resize(h->P);
+  auto bail = [&](int code) {
+    ewh_destroy(h);
+    return code;
+  };
+  if (hipStreamCreateWithFlags(&h->stream, hipStreamNonBlocking) != hipSuccess)
+    return bail(set_err(EWH_E_HIP, "hipStreamCreate failed"));
+  bool any_theta_white = false;
+  for (int p = 0; p < h->P; ++p) {
+    const ewh_pulsar_desc& s = d->pulsars[p];
+    PsrHost& ps = h->psr[p];
+    ps.n_toa = s.n_toa;
+    ps.m = s.n_col;
+    ps.nlead = s.n_lead_const;
+    ps.nb = nb_for(s.n_col + 1);
+    ps.ld = 16 * ps.nb;
+    ps.n_epoch = s.n_epoch;
+    ps.fx_m = s.n_col - s.n_lead_const;
+    ps.fx_nb = nb_for(ps.fx_m + 1);
+    ps.fx_ld = 16 * ps.fx_nb;
+    for (int i = 0; i < s.n_slot; ++i) ps.has_theta_white |= pref_uses_theta(s.slots[i]);
+    any_theta_white |= ps.has_theta_white;
+    // T_aug: [basis | 0-pad | r], row-major n x ld
+    std::vector<double> Ta((size_t)s.n_toa * ps.ld, 0.0), sig2(s.n_toa);
+    for (int t = 0; t < s.n_toa; ++t) {
+      for (int j = 0; j < s.n_col; ++j) Ta[(size_t)t * ps.ld + j] = s.basis[(size_t)t * s.n_col + j];
+      Ta[(size_t)t * ps.ld + ps.ld - 1] = s.resid[t];
+      sig2[t] = s.toaerr[t] * s.toaerr[t];
+    }
+    double* dT;
+    double* dsig2;
+    int *d_ef, *d_eq, *d_es, *d_ee, *d_eslot;
+    ewh_pref* d_slots;
+    if ((rc = dupload(h, &dT, Ta.data(), Ta.size()))) return bail(rc);
+    if ((rc = dupload(h, &dsig2, sig2.data(), sig2.size()))) return bail(rc);
+    if ((rc = dupload(h, &d_ef, s.efac_slot, (size_t)s.n_toa))) return bail(rc);
+    if ((rc = dupload(h, &d_eq, s.equad_slot, (size_t)s.n_toa))) return bail(rc);
+    if ((rc = dupload(h, &d_slots, s.slots, (size_t)s.n_slot))) return bail(rc);
+    if ((rc = dupload(h, &d_es, s.epoch_start, (size_t)s.n_epoch))) return bail(rc);
+    if ((rc = dupload(h, &d_ee, s.epoch_stop, (size_t)s.n_epoch))) return bail(rc);
+    if ((rc = dupload(h, &d_eslot, s.epoch_slot, (size_t)s.n_epoch))) return bail(rc);
+    ps.dev = PsrDev{s.n_toa, s.n_col, ps.ld, ps.nb, s.n_epoch, dT, dsig2, d_ef, d_eq, d_slots, d_es, d_ee, d_eslot};
+    std::vector<int> ptr;
+    std::vector<ewh_spec_entry> ent;
+    build_csr(s, 0, s.n_col, ptr, ent);
+    if ((rc = dupload(h, &ps.d_colptr, ptr.data(), ptr.size()))) return bail(rc);
+    if ((rc = dupload(h, &ps.d_spec, ent.data(), ent.size()))) return bail(rc);
+    build_csr(s, s.n_lead_const, s.n_col, ptr, ent);
+    if ((rc = dupload(h, &ps.d_fx_colptr, ptr.data(), ptr.size()))) return bail(rc);
+    if ((rc = dupload(h, &ps.d_fx_spec, ent.data(), ent.size()))) return bail(rc);
+  }
+  h->white_fixed = (d->white_fixed != 0) && !any_theta_white;
+  if ((rc = dalloc(h, &h->d_jobs_fixed, h->P))) return bail(rc);
+  if ((rc = dalloc(h, &h->d_jobs_var, h->P))) return bail(rc);
+  if (h->white_fixed) {
+    if ((rc = setup_fixed(h, d))) return bail(rc);
+  }
+  *out = h;
+  return 0;
+}
+
+int ewh_set_kernel_mode(ewh_handle* h, int32_t mode) {
+  if (!h || mode < 0 || mode > 1) return set_err(EWH_E_INVALID, "bad handle / mode");
+  h->kernel_mode = mode;
+  return 0;
+}
+
+double ewh_unit_cost(const ewh_handle* h, int32_t p) {
+  if (!h || p < 0 || p >= h->P) return 0.0;
+  const PsrHost& ps = h->psr[p];
+  if (h->white_fixed) return (double)ps.fx_ld * ps.fx_ld * ps.fx_ld / 3.0;
+  return (double)ps.n_toa * ps.ld * ps.ld + (double)ps.ld * ps.ld * ps.ld / 3.0;
+}
+
+int ewh_lnl_units_device(ewh_handle* h, const double* theta_dev, int32_t B, int64_t u_begin, int64_t u_end,
+                         double* out_dev, void* stream) {
+  if (!h || !theta_dev || !out_dev || B <= 0) return set_err(EWH_E_INVALID, "bad arguments");
+  const long long U = (long long)h->P * B;
+  u_begin = std::max<int64_t>(0, u_begin);
+  u_end = std::min<int64_t>(U, u_end);
+  EWH_HIP(hipSetDevice(h->device));
+  hipStream_t st = stream ? (hipStream_t)stream : h->stream;
+  int rc;
+  if ((rc = ensure_units(h, B))) return rc;
+  EWH_HIP(hipMemsetAsync(h->d_units, 0, sizeof(double) * (size_t)h->P * B, st));
+  const int ldth = h->n_param;
+  hipStream_t saved = h->stream;
+  h->stream = st;
+  if (h->white_fixed) {
+    // one launch per run of consecutive pulsars with the same kernel class
+    long long u = u_begin;
+    while (u < u_end) {
+      const int p0 = (int)(u / B);
+      const int nb0 = h->psr[p0].fx_nb;
+      int p1 = p0 + 1;
+      while (p1 < h->P && h->psr[p1].fx_nb == nb0 && (long long)p1 * B < u_end) ++p1;
+      const long long seg_end = std::min<long long>(u_end, (long long)p1 * B);
+      int maxm = 0;
+      for (int p = p0; p < p1; ++p) maxm = std::max(maxm, h->psr[p].fx_m);
+      if ((rc = dispatch_chol(h->kernel_mode, nb0, maxm, h->d_jobs_fixed, B, u, seg_end - u, 0, theta_dev, ldth,
+                              h->d_units, st))) {
+        h->stream = saved;
+        return rc;
+      }
+      u = seg_end;
+    }
+  } else {
+    if ((rc = ensure_var_scratch(h, B))) {
+      h->stream = saved;
+      return rc;
+    }
+    for (long long u = u_begin; u < u_end;) {
+      const int p = (int)(u / B);
+      const long long pend = std::min<long long>(u_end, (long long)(p + 1) * B);
+      const int bs = (int)(u - (long long)p * B), be = (int)(pend - (long long)p * B);
+      for (int c0 = bs; c0 < be; c0 += h->chunk) {
+        const int nb = std::min(h->chunk, be - c0);
+        if ((rc = run_white(h, p, theta_dev, ldth, c0, nb))) {
+          h->stream = saved;
+          return rc;
+        }
+        if ((rc = dispatch_chol(h->kernel_mode, h->psr[p].nb, h->psr[p].m, h->d_jobs_var, B,
+                                (long long)p * B + c0, nb, c0, theta_dev, ldth, h->d_units, st))) {
+          h->stream = saved;
+          return rc;
+        }
+      }
+      u = pend;
+    }
+  }
+  h->stream = saved;
+  hipLaunchKernelGGL(reduce_units_kernel, dim3((B + 255) / 256), dim3(256), 0, st, h->d_units, h->P, B, out_dev);
+  EWH_HIP(hipGetLastError());
+  h->last_B = B;
+  return 0;
+}
+
+int ewh_lnl_batch(ewh_handle* h, const double* theta_host, int32_t B, double* out_host) {
+  if (!h || !theta_host || !out_host || B <= 0) return set_err(EWH_E_INVALID, "bad arguments");
+  EWH_HIP(hipSetDevice(h->device));
+  const size_t need = (size_t)B * std::max(1, h->n_param) + B;
+  if (need > h->io_cap) {
+    for (void* p : {(void*)h->d_theta}) {
+      if (p) {
+        hipFree(p);
+        h->allocs.erase(std::find(h->allocs.begin(), h->allocs.end(), p));
+      }
+    }
+    h->io_cap = 0;
+    int rc = dalloc(h, &h->d_theta, need);
+    if (rc) return rc;
+    h->io_cap = need;
+  }
+  h->d_out = h->d_theta + (size_t)B * std::max(1, h->n_param);
+  if (h->n_param > 0)
+    EWH_HIP(hipMemcpyAsync(h->d_theta, theta_host, sizeof(double) * (size_t)B * h->n_param, hipMemcpyHostToDevice,
+                           h->stream));
+  int rc = ewh_lnl_units_device(h, h->d_theta, B, 0, (long long)h->P * B, h->d_out, h->stream);
+  if (rc) return rc;
+  EWH_HIP(hipMemcpyAsync(out_host, h->d_out, sizeof(double) * B, hipMemcpyDeviceToHost, h->stream));
+  EWH_HIP(hipStreamSynchronize(h->stream));
+  return 0;
+}
+
+int ewh_last_unit_terms(ewh_handle* h, double* out_host, int32_t B) {
+  if (!h || !out_host || B != h->last_B || !h->d_units) return set_err(EWH_E_INVALID, "no matching previous call");
+  EWH_HIP(hipSetDevice(h->device));
+  EWH_HIP(hipStreamSynchronize(h->stream));
+  EWH_HIP(hipDeviceSynchronize());
+  EWH_HIP(hipMemcpy(out_host, h->d_units, sizeof(double) * (size_t)h->P * B, hipMemcpyDeviceToHost));
+  return 0;
+}
+
+void ewh_destroy(ewh_handle* h) {
+  if (!h) return;
+  hipSetDevice(h->device);
+  if (h->stream) hipStreamSynchronize(h->stream);
+  for (void* p : h->allocs) hipFree(p);
+  if (h->stream) hipStreamDestroy(h->stream);
+  delete h;
+}
+
+}  // extern "C"

@@ -1,0 +1,318 @@
+"""`PTA`: the drop-in for enterprise's `signal_base.PTA` on the likelihood path.
+
+Reference boundary: `pta = signal_base.PTA(models)` (enterprise_warp.py:502),
+`pta.set_default_params(noisedict)` (:508), `pta.param_names` (:511, :515),
+`pta.params` (bilby_warp.py:51; run_example_paramfile.py:29) and
+`pta.get_lnlikelihood(params)` with a dict (bilby_warp.py:35) or an ndarray in
+`param_names` order (PTSampler via run_example_paramfile.py:27-30).
+
+Every likelihood call goes to libewarp_hip.so (hand-written gfx950 kernels)
+through the C ABI in include/ewarp_hip.h; there is no CPU path.  New in this
+framework: `get_lnlikelihood_batch(X[B, nparam])` evaluates a batch of sampler
+proposals in one device call, and `engine()` exposes the device-pointer entry
+used for multi-GPU sharding (bench.py, enterprise_warp_amd/sharding.py).
+"""
+import ctypes as C
+
+import numpy as np
+
+from . import _lib
+from . import constants as const
+from . import parameter as parameter
+from .signals import SignalCollection
+
+
+class PTA:
+    def __init__(self, init, lnlikelihood=None):
+        if isinstance(init, SignalCollection):
+            init = [init]
+        self._collections = list(init)
+        names = [c.name for c in self._collections]
+        if len(set(names)) != len(names):
+            raise ValueError("duplicate pulsar names in PTA")
+        self._engine = None
+        self._engine_device = None
+        self._rebuild_params()
+
+    # ------------------------------------------------------------------ params
+    def _rebuild_params(self):
+        allp = {}
+        for c in self._collections:
+            for p in c.all_params:
+                q = allp.setdefault(p.name, p)
+                if q is not p and type(q) is not type(p):
+                    raise ValueError(f"parameter {p.name} defined with two different priors")
+        self._all = allp
+        self._params = [allp[k] for k in sorted(allp) if not isinstance(allp[k], parameter.ConstantParameter)]
+        self._index = {}
+        ct = 0
+        for p in self._params:
+            n = p.size if p.size else 1
+            self._index[p.name] = ct
+            ct += n
+        self._nparam = ct
+
+    @property
+    def params(self):
+        return list(self._params)
+
+    @property
+    def param_names(self):
+        out = []
+        for p in self._params:
+            if p.size:
+                out.extend(f"{p.name}_{i}" for i in range(p.size))
+            else:
+                out.append(p.name)
+        return out
+
+    @property
+    def pulsars(self):
+        return [c.name for c in self._collections]
+
+    @property
+    def signal_collections(self):
+        return list(self._collections)
+
+    def map_params(self, xs):
+        """ndarray in param_names order -> {name: value} ([ent] PTA.map_params)."""
+        xs = np.asarray(xs, dtype=float)
+        ret, ct = {}, 0
+        for p in self._params:
+            n = p.size if p.size else 1
+            ret[p.name] = xs[ct:ct + n] if n > 1 else float(xs[ct])
+            ct += n
+        return ret
+
+    def set_default_params(self, params):
+        """Set Constant values from a noise dictionary (enterprise_warp.py:504-508).
+
+        Compatibility alias: the reference's example
+        noise files name EQUAD `{psr}_{backend}_log10_equad` while
+        TNEquadNoise's parameter is `..._log10_tnequad`; a `_log10_equad` key
+        fills the matching `_log10_tnequad` Constant when that key is absent."""
+        changed = False
+        keyed = dict(params)
+        for k, v in params.items():
+            if k.endswith("_log10_equad"):
+                keyed.setdefault(k[: -len("_log10_equad")] + "_log10_tnequad", v)
+        for p in self._all.values():
+            if isinstance(p, parameter.ConstantParameter) and p.name in keyed:
+                val = float(keyed[p.name])
+                if p.value != val:
+                    p.value = val
+                    changed = True
+        if changed:
+            self._drop_engine()
+
+    def get_lnprior(self, params):
+        d = params if isinstance(params, dict) else self.map_params(params)
+        return float(sum(p.get_logpdf(d[p.name]) for p in self._params))
+
+    def _theta(self, X):
+        """dict / ndarray / batch -> theta matrix [B, nparam] (param_names order)."""
+        if isinstance(X, dict):
+            row = np.empty(self._nparam)
+            for p in self._params:
+                i = self._index[p.name]
+                if p.name in X:
+                    v = np.atleast_1d(np.asarray(X[p.name], dtype=float))
+                elif p.size and all(f"{p.name}_{j}" in X for j in range(p.size)):
+                    v = np.array([X[f"{p.name}_{j}"] for j in range(p.size)], dtype=float)
+                else:
+                    raise KeyError(f"missing value for parameter {p.name}")
+                row[i:i + (p.size or 1)] = v
+            return row[None, :]
+        X = np.asarray(X, dtype=float)
+        if X.ndim == 1:
+            X = X[None, :]
+        if X.shape[1] != self._nparam:
+            raise ValueError(f"expected {self._nparam} parameters per sample, got {X.shape[1]}")
+        return np.ascontiguousarray(X)
+
+    # -------------------------------------------------------------- likelihood
+    def get_lnlikelihood(self, params, **kwargs):
+        return float(self.get_lnlikelihood_batch(self._theta(params))[0])
+
+    def get_lnlikelihood_batch(self, X):
+        th = self._theta(X)
+        return self.engine().lnl_batch(th)
+
+    def engine(self, device=None):
+        """The device-resident likelihood (created on first use, after
+        set_default_params; re-created when constants change)."""
+        if device is None:
+            device = self._engine_device if self._engine_device is not None else 0
+        if self._engine is None or self._engine_device != device:
+            self._drop_engine()
+            self._engine = Engine(self, device)
+            self._engine_device = device
+        return self._engine
+
+    def _drop_engine(self):
+        if self._engine is not None:
+            self._engine.close()
+        self._engine = None
+
+    # ----------------------------------------------------------------- layout
+    def _pref(self, p, elem=None):
+        if isinstance(p, parameter.ConstantParameter):
+            if p.value is None:
+                raise ValueError(f"Constant parameter {p.name} has no value: call set_default_params "
+                                 "(noise files) first")
+            return (-1, float(p.value))
+        return (self._index[p.name] + (elem or 0), 0.0)
+
+    def white_fixed(self):
+        return all(isinstance(p, parameter.ConstantParameter)
+                   for c in self._collections for w in c.white for p in w.params)
+
+    def layout(self):
+        """Host-side per-pulsar tables for the engine (plain numpy)."""
+        out = []
+        for c in self._collections:
+            psr = c.psr
+            n = len(psr.toas)
+            slots, slot_of = [], {}
+
+            def slot(p):
+                if p.name not in slot_of:
+                    slot_of[p.name] = len(slots)
+                    slots.append(self._pref(p))
+                return slot_of[p.name]
+
+            efac = np.full(n, -1, np.int32)
+            equad = np.full(n, -1, np.int32)
+            for w in c.white:
+                if w.kind == "ecorr":
+                    continue
+                tgt = efac if w.kind == "efac" else equad
+                for key, mask in w.masks.items():
+                    tgt[mask] = slot(w.pars[key])
+            if np.any(efac < 0):
+                raise ValueError(f"{c.name}: some TOAs are not covered by the efac selection")
+            eps = c.ecorr_epochs()
+            ep_start = np.array([e[0] for e in eps], np.int32)
+            ep_stop = np.array([e[1] for e in eps], np.int32)
+            ep_slot = np.array([slot(e[2]) for e in eps], np.int32)
+            spec = []
+            for j, ents in enumerate(c.entries):
+                for e in ents:
+                    if e["kind"] == "const":
+                        spec.append((_lib.SPEC_CONST, j, (-1, e["value"]), (-1, 0.0), (-1, 0.0), 0.0, 0.0))
+                    elif e["kind"] == "powerlaw":
+                        pa = e["pars"]
+                        spec.append((_lib.SPEC_POWERLAW, j, self._pref(pa["log10_A"]), self._pref(pa["gamma"]),
+                                     (-1, 0.0), e["f"], e["df"]))
+                    elif e["kind"] == "turnover":
+                        pa = e["pars"]
+                        spec.append((_lib.SPEC_TURNOVER, j, self._pref(pa["log10_A"]), self._pref(pa["gamma"]),
+                                     self._pref(pa["fc"]), e["f"], e["df"]))
+                    elif e["kind"] == "free_spectrum":
+                        p = e["pars"]["log10_rho"]
+                        if isinstance(p, parameter.ConstantParameter):
+                            vals = np.atleast_1d(p.value)
+                            ref = (-1, float(vals[e["mode"]] if len(vals) > 1 else vals[0]))
+                        else:
+                            ref = self._pref(p, e["mode"])
+                        spec.append((_lib.SPEC_FREESPEC, j, ref, (-1, 0.0), (-1, 0.0), e["f"], 0.0))
+                    else:
+                        raise ValueError(e["kind"])
+            out.append(dict(name=c.name, T=np.ascontiguousarray(c.T, dtype=float),
+                            resid=np.ascontiguousarray(psr.residuals, dtype=float),
+                            toaerr=np.ascontiguousarray(psr.toaerrs, dtype=float),
+                            n_lead=c.n_lead_const, slots=slots, efac=efac, equad=equad,
+                            ep_start=ep_start, ep_stop=ep_stop, ep_slot=ep_slot, spec=spec))
+        return out
+
+    # ---------------------------------------------------------------- helpers
+    def constant_values(self):
+        return {p.name: p.value for p in self._all.values() if isinstance(p, parameter.ConstantParameter)}
+
+    def oracle_terms(self):
+        return [c.oracle_terms() for c in self._collections]
+
+    def summary(self):
+        lines = [f"PTA with {len(self._collections)} pulsars, {self._nparam} free parameters"]
+        for c in self._collections:
+            lines.append(f"  {c.name}: n_toa={len(c.psr.toas)} basis={c.T.shape[1]} (tm {c.n_lead_const}) "
+                         f"white={[w.kind for w in c.white]}")
+        return "\n".join(lines)
+
+    def __repr__(self):
+        return self.summary()
+
+
+def _as_ptr(a, ctype):
+    return a.ctypes.data_as(C.POINTER(ctype))
+
+
+class Engine:
+    """Owner of one libewarp_hip handle (one device)."""
+
+    def __init__(self, pta, device=0):
+        self.lib = _lib.load()
+        self.pta = pta
+        self.device = device
+        lay = pta.layout()
+        self.n_pulsar = len(lay)
+        self.n_param = pta._nparam
+        keep = []
+        descs = (_lib.PulsarDesc * len(lay))()
+        for i, L in enumerate(lay):
+            n, m = L["T"].shape
+            slots = (_lib.Pref * max(1, len(L["slots"])))()
+            for k, (idx, cv) in enumerate(L["slots"]):
+                slots[k] = _lib.Pref(idx, 0, cv)
+            spec = (_lib.SpecEntry * max(1, len(L["spec"])))()
+            for k, (kind, col, p0, p1, p2, f, df) in enumerate(L["spec"]):
+                spec[k] = _lib.SpecEntry(kind, col, _lib.Pref(p0[0], 0, p0[1]), _lib.Pref(p1[0], 0, p1[1]),
+                                         _lib.Pref(p2[0], 0, p2[1]), f, df, const.fyr)
+            arrs = [L["T"], L["resid"], L["toaerr"], L["efac"], L["equad"], L["ep_start"], L["ep_stop"],
+                    L["ep_slot"]]
+            keep.extend(arrs + [slots, spec])
+            descs[i] = _lib.PulsarDesc(
+                n, m, L["n_lead"], len(L["spec"]),
+                _as_ptr(L["T"], C.c_double), _as_ptr(L["resid"], C.c_double), _as_ptr(L["toaerr"], C.c_double),
+                len(L["slots"]), slots, _as_ptr(L["efac"], C.c_int32), _as_ptr(L["equad"], C.c_int32),
+                len(L["ep_start"]), _as_ptr(L["ep_start"], C.c_int32), _as_ptr(L["ep_stop"], C.c_int32),
+                _as_ptr(L["ep_slot"], C.c_int32), spec)
+        self.white_fixed = pta.white_fixed()
+        d = _lib.PtaDesc(_lib.EWH_ABI_VERSION, len(lay), self.n_param, int(self.white_fixed), descs)
+        h = C.c_void_p()
+        _lib.check(self.lib.ewh_create(C.byref(d), int(device), C.byref(h)))
+        self.h = h
+        del keep
+
+    def lnl_batch(self, theta):
+        theta = np.ascontiguousarray(theta, dtype=float)
+        B = theta.shape[0]
+        out = np.empty(B)
+        _lib.check(self.lib.ewh_lnl_batch(self.h, _as_ptr(theta, C.c_double), B, _as_ptr(out, C.c_double)))
+        return out
+
+    def lnl_units_device(self, theta_ptr, B, u0, u1, out_ptr, stream=None):
+        _lib.check(self.lib.ewh_lnl_units_device(self.h, C.c_void_p(theta_ptr), int(B), int(u0), int(u1),
+                                                 C.c_void_p(out_ptr), C.c_void_p(stream or 0)))
+
+    def unit_terms(self, B):
+        out = np.empty((self.n_pulsar, B))
+        _lib.check(self.lib.ewh_last_unit_terms(self.h, _as_ptr(out, C.c_double), int(B)))
+        return out
+
+    def unit_costs(self):
+        return np.array([self.lib.ewh_unit_cost(self.h, p) for p in range(self.n_pulsar)])
+
+    def set_kernel_mode(self, mode):
+        _lib.check(self.lib.ewh_set_kernel_mode(self.h, int(mode)))
+
+    def close(self):
+        if getattr(self, "h", None):
+            self.lib.ewh_destroy(self.h)
+            self.h = None
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass

@@ -1,0 +1,157 @@
+/*
+ * ewarp_hip.h — C ABI of libewarp_hip.so, the MI355X (gfx950) PTA
+ * log-likelihood engine behind enterprise_warp_amd.PTA.
+ *
+ * Drop-in boundary.  In the reference the likelihood is the object built by
+ * `signal_base.PTA(models)` at enterprise_warp.py:502 and called as
+ * `pta.get_lnlikelihood(params)` at bilby_warp.py:35 (and, through
+ * enterprise_extensions' PTSampler, with an ndarray at
+ * examples/run_example_paramfile.py:27-30).  The Python class
+ * enterprise_warp_amd.pta.PTA keeps that surface and binds these entry
+ * points with ctypes.
+ *
+ *   ewh_create          replaces signal_base.PTA.__init__ + the white-noise
+ *                       cache of LogLikelihood (enterprise_warp.py:502-508):
+ *                       uploads every pulsar's basis, residuals, TOA errors,
+ *                       white-noise tables and spectral table; when white
+ *                       noise is fixed (Constant efac/equad/ecorr set from
+ *                       noise files, enterprise_warp.py:504-508) it also
+ *                       computes and caches T^T N^-1 T, T^T N^-1 r, r^T N^-1 r,
+ *                       log|N| and the timing-model elimination on device.
+ *   ewh_lnl_batch       replaces B calls of pta.get_lnlikelihood
+ *                       (bilby_warp.py:35) — host theta in, host lnL out.
+ *   ewh_lnl_units_device  the same on device buffers for a contiguous range
+ *                       of (pulsar, sample) units; used for multi-GPU
+ *                       sharding (partial sums, then an RCCL all-reduce).
+ *   ewh_destroy / ewh_last_error / ewh_version: lifecycle and errors.
+ *
+ * Conventions
+ *  - theta is row-major [B x n_param] float64, column order = the caller's
+ *    parameter order (enterprise_warp_amd.PTA.param_names).
+ *  - A parameter reference (ewh_pref) is either a column of theta (idx >= 0)
+ *    or a constant (idx < 0, value cval).
+ *  - Ownership: the caller owns every host buffer for the duration of the
+ *    call; the library copies what it needs and keeps no caller pointer.
+ *    The library owns every device buffer it allocates (freed in destroy).
+ *  - Errors: 0 on success, negative EWH_E* code otherwise; the message is in
+ *    the thread-local ewh_last_error().  A failed Cholesky for a sample is
+ *    NOT an error: its lnL is -INFINITY (enterprise: LinAlgError -> -np.inf).
+ *  - Threads: one handle per host thread (no internal locking).  The HIP
+ *    context is touched only inside ewh_create and later calls, never at
+ *    library load, so forked sampler workers stay safe.
+ */
+#ifndef EWARP_HIP_H
+#define EWARP_HIP_H
+
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define EWH_ABI_VERSION 1
+
+enum ewh_status {
+  EWH_OK = 0,
+  EWH_E_INVALID = -1,   /* bad descriptor / argument */
+  EWH_E_HIP = -2,       /* HIP runtime error */
+  EWH_E_NOMEM = -3,     /* device allocation failed */
+  EWH_E_UNSUPPORTED = -4
+};
+
+/* Spectral-entry kinds: phi contribution of one basis column.
+ *  POWERLAW  [ent] utils.powerlaw      p0 = log10_A, p1 = gamma           (enterprise_models.py:180)
+ *  TURNOVER  powerlaw_bpl              p0 = log10_A, p1 = gamma, p2 = fc  (enterprise_models.py:553-563)
+ *  FREESPEC  [ent] free_spectrum       p0 = log10_rho[j]                  (enterprise_models.py:388)
+ *  CONST     phi = p0.cval (timing model: 1e40, [ent] utils.tm_prior)
+ * Entries of merged columns ([ent] SignalCollection._combine_basis_columns)
+ * are summed, as enterprise's KernelMatrix.add does. */
+enum ewh_spec_kind {
+  EWH_SPEC_POWERLAW = 1,
+  EWH_SPEC_TURNOVER = 2,
+  EWH_SPEC_FREESPEC = 3,
+  EWH_SPEC_CONST = 4
+};
+
+typedef struct ewh_pref {
+  int32_t idx;   /* >= 0: theta column; < 0: constant */
+  int32_t pad_;
+  double cval;
+} ewh_pref;
+
+typedef struct ewh_spec_entry {
+  int32_t kind;  /* ewh_spec_kind */
+  int32_t col;   /* basis column 0..n_col-1 */
+  ewh_pref p0, p1, p2;
+  double f;      /* Fourier frequency (1/s) */
+  double df;     /* np.diff(concatenate([0], f[::2])) entry, as [ent] powerlaw */
+  double fyr;    /* 1 / Julian year (s^-1), [ent] constants.fyr */
+} ewh_spec_entry;
+
+/* One pulsar's data and model tables.  TOAs are sorted; ECORR epochs are
+ * contiguous TOA slices ([ent] utils.quant2ind). */
+typedef struct ewh_pulsar_desc {
+  int32_t n_toa;
+  int32_t n_col;          /* basis columns after merging */
+  int32_t n_lead_const;   /* leading columns whose phi is constant (timing model) */
+  int32_t n_spec;
+  const double* basis;    /* n_toa x n_col, row-major */
+  const double* resid;    /* n_toa, seconds */
+  const double* toaerr;   /* n_toa, seconds */
+  /* white noise: N_t = efac^2 sigma_t^2 + 10^(2 log10_tnequad) (+ ECORR blocks) */
+  int32_t n_slot;         /* size of the white-noise parameter table */
+  const ewh_pref* slots;  /* n_slot */
+  const int32_t* efac_slot;   /* n_toa: slot of efac (MeasurementNoise) */
+  const int32_t* equad_slot;  /* n_toa: slot of log10_tnequad, -1 = none */
+  int32_t n_epoch;
+  const int32_t* epoch_start; /* n_epoch, first TOA of the epoch */
+  const int32_t* epoch_stop;  /* n_epoch, one past the last TOA */
+  const int32_t* epoch_slot;  /* n_epoch: slot of log10_ecorr */
+  const ewh_spec_entry* spec; /* n_spec */
+} ewh_pulsar_desc;
+
+typedef struct ewh_pta_desc {
+  int32_t abi_version;    /* EWH_ABI_VERSION */
+  int32_t n_pulsar;
+  int32_t n_param;        /* theta row length */
+  int32_t white_fixed;    /* 1: no white-noise slot references theta -> cache TNT */
+  const ewh_pulsar_desc* pulsars;
+} ewh_pta_desc;
+
+typedef struct ewh_handle ewh_handle;
+
+/* Build the device-resident PTA on HIP device `device`. */
+int ewh_create(const ewh_pta_desc* desc, int device, ewh_handle** out);
+
+/* lnL for B samples: theta_host [B x n_param], out_host [B]. Synchronous. */
+int ewh_lnl_batch(ewh_handle* h, const double* theta_host, int32_t B, double* out_host);
+
+/* Device variant on a contiguous range [unit_begin, unit_end) of units
+ * u = pulsar * B + sample.  out_dev[b] = sum of the unit lnL terms of sample
+ * b inside the range (0 where the range has none).  Asynchronous on `stream`
+ * (a hipStream_t; NULL = the default stream).  theta_dev and out_dev are
+ * device pointers. */
+int ewh_lnl_units_device(ewh_handle* h, const double* theta_dev, int32_t B,
+                         int64_t unit_begin, int64_t unit_end, double* out_dev,
+                         void* stream);
+
+/* Per-pulsar lnL terms of the last call: out_host [n_pulsar x B] (row p =
+ * pulsar p).  Units outside the last range read 0. Synchronous. */
+int ewh_last_unit_terms(ewh_handle* h, double* out_host, int32_t B);
+
+/* Cost model used for sharding: relative cost of one unit of pulsar p. */
+double ewh_unit_cost(const ewh_handle* h, int32_t pulsar);
+
+/* Kernel selection: 0 = auto (MFMA register-blocked Cholesky when the
+ * reduced matrix fits, LDS kernel otherwise), 1 = force the LDS kernel. */
+int ewh_set_kernel_mode(ewh_handle* h, int32_t mode);
+
+void ewh_destroy(ewh_handle* h);
+const char* ewh_last_error(void);
+int ewh_version(void);
+
+#ifdef __cplusplus
+}
+#endif
+
+#endif /* EWARP_HIP_H */

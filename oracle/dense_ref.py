@@ -1,0 +1,53 @@
+"""TEST INFRASTRUCTURE ONLY — brute-force dense Gaussian lnL.
+
+Independent of the Woodbury / Sherman-Morrison route in enterprise_ref: builds
+the full n x n covariance C = N + U J U^T + T phi T^T explicitly and evaluates
+-1/2 r^T C^{-1} r - 1/2 log|C| with a dense Cholesky.  The timing-model prior
+must be finite here (phi_tm = tm_var, e.g. 1e-12 s^2), because phi_tm = 1e40
+cannot be represented densely.
+
+Relation to enterprise's convention: enterprise omits
+-1/2 n log 2pi, so `dense_lnl` omits it too; the Woodbury form equals
+-1/2 r^T C^-1 r - 1/2 log|C| exactly, so for the same finite phi_tm the two
+agree to rounding.
+"""
+import numpy as np
+import scipy.linalg as sl
+
+
+def dense_lnl(oracle_pulsar, params, tm_var=None):
+    """lnL of one pulsar from the dense covariance.
+
+    oracle_pulsar: enterprise_ref.OraclePulsar; tm_var overrides phi of the
+    timing-model columns (required when the model has a timing model)."""
+    pp = oracle_pulsar
+    D, ep = pp._sm(params)
+    n = len(D)
+    C = np.diag(D)
+    for slc, jv in ep:
+        C[slc, slc] += jv
+    phi = pp.phi(params)
+    if tm_var is not None:
+        for g in pp.gps:
+            if g["kind"] == "tm":
+                phi[g["idx"]] = tm_var
+    C += (pp.T * phi[None, :]) @ pp.T.T
+    cf = sl.cho_factor(C, lower=True)
+    x = sl.cho_solve(cf, pp.r)
+    return -0.5 * np.dot(pp.r, x) - np.sum(np.log(np.diag(cf[0])))
+
+
+def woodbury_lnl(oracle_pulsar, params, tm_var=None):
+    """The same pulsar through the enterprise route, with phi_tm = tm_var."""
+    pp = oracle_pulsar
+    TNT, TNr, rNr, ldN = pp.white_terms(params)
+    phi = pp.phi(params)
+    if tm_var is not None:
+        for g in pp.gps:
+            if g["kind"] == "tm":
+                phi[g["idx"]] = tm_var
+    Sigma = TNT + np.diag(1.0 / phi)
+    cf = sl.cho_factor(Sigma)
+    expval = sl.cho_solve(cf, TNr)
+    return (-0.5 * (rNr + ldN)
+            + 0.5 * (TNr @ expval - 2 * np.sum(np.log(np.diag(cf[0]))) - np.sum(np.log(phi))))

@@ -1,0 +1,110 @@
+"""CPU tests of the oracle: known answers, dense cross-check, golden vectors."""
+import os
+
+import numpy as np
+import pytest
+
+from conftest import GOLDEN_NAMES, REF_EXAMPLES, load_golden
+from enterprise_warp_amd import constants as const
+from enterprise_warp_amd import synth
+from enterprise_warp_amd.pulsar import pulsar_from_par_tim
+from enterprise_warp_amd.models import StandardModels
+from oracle import enterprise_ref as ref
+from oracle.dense_ref import dense_lnl, woodbury_lnl
+
+
+def oracle_for(pta, fixed=False):
+    const_ = pta.constant_values()
+    return ref.OraclePTA([c.psr for c in pta.signal_collections], pta.oracle_terms(),
+                         fixed_params=const_ if fixed else None)
+
+
+def test_white_only_closed_form():
+    """efac = 1, no GP: lnL = -1/2 sum(r^2/sigma^2 + log sigma^2)."""
+    rng = np.random.default_rng(0)
+    psr = synth.make_pulsar("J0001", 200, seed=1)
+    psr.residuals = rng.standard_normal(200) * psr.toaerrs
+    o = ref.OraclePTA([psr], [[{"kind": "efac", "selection": "no_selection"}]])
+    got = o.lnlikelihood({f"{psr.name}_efac": 1.0})
+    want = -0.5 * np.sum(psr.residuals ** 2 / psr.toaerrs ** 2 + np.log(psr.toaerrs ** 2))
+    assert abs(got - want) <= 1e-9 * abs(want)
+
+
+def test_powerlaw_known_values():
+    f = np.repeat(np.array([1.0, 2.0, 3.0]) / (10 * const.yr), 2)
+    v = ref.powerlaw(f, -14.0, 13.0 / 3.0)
+    df = 1.0 / (10 * const.yr)
+    want = 1e-28 / (12 * np.pi ** 2) * const.fyr ** (13 / 3 - 3) * f ** (-13 / 3) * df
+    np.testing.assert_allclose(v, want, rtol=1e-13)
+    # free spectrum: 10^(2 rho) repeated for sin/cos
+    np.testing.assert_allclose(ref.free_spectrum(f, [-7.0, -8.0, -9.0]), np.repeat([1e-14, 1e-16, 1e-18], 2))
+    # turnover with fc < 0 means lg fc (enterprise_models.py:561)
+    a = ref.powerlaw_bpl(f, -14.0, 4.0, -8.0)
+    b = ref.powerlaw_bpl(f, -14.0, 4.0, 1e-8)
+    np.testing.assert_allclose(a, b, rtol=1e-14)
+
+
+def test_hd_orf_known_values():
+    from enterprise_warp_amd.models import hd_orf, hd_orf_noauto
+    z = np.array([0.0, 0.0, 1.0])
+    assert hd_orf(z, z) == 1.0 and hd_orf_noauto(z, z) == 0.0
+    x90 = np.array([1.0, 0.0, 0.0])
+    # zeta = 90 deg: x = 1/2 -> 1.5 x ln x - x/4 + 1/2
+    np.testing.assert_allclose(hd_orf(z, x90), 0.75 * np.log(0.5) - 0.125 + 0.5)
+    # zeta = 180 deg: x = 1 -> 0.25
+    np.testing.assert_allclose(hd_orf(z, -z), 0.25)
+
+
+@pytest.mark.parametrize("tim,expect", [("J1832-0836", 32), ("fake_psr_0", 60)])
+def test_determine_nfreqs_reference_rule(tim, expect):
+    """enterprise_models.py:457-462 on the reference's example pulsars."""
+    d = os.path.join(REF_EXAMPLES, "data")
+    psr = pulsar_from_par_tim(os.path.join(d, tim + ".par"), os.path.join(d, tim + ".tim"))
+    ns = synth.params_namespace(psr.toas.max() - psr.toas.min(), False)
+    assert StandardModels(psr=psr, params=ns).determine_nfreqs() == expect
+
+
+def test_quantization_rule():
+    t = np.array([0.0, 0.5, 0.9, 1.0, 1.2, 5.0, 9.0, 9.5])
+    b = ref.quantization_slices(t)
+    assert [list(x) for x in b] == [[0, 1, 2], [3, 4], [6, 7]]
+
+
+@pytest.mark.parametrize("tm_var", [1e-12, 1e-14])
+def test_woodbury_matches_dense(tm_var):
+    """SM / Woodbury route == brute-force dense covariance (finite TM prior)."""
+    c = synth.config_c2(n_toa=600)
+    o = oracle_for(c.pta)
+    pp = o.pulsars[0]
+    a = dense_lnl(pp, c.truth, tm_var=tm_var)
+    b = woodbury_lnl(pp, c.truth, tm_var=tm_var)
+    assert abs(a - b) <= 1e-10 * abs(a)
+
+
+@pytest.mark.parametrize("name", GOLDEN_NAMES)
+def test_oracle_reproduces_golden(name):
+    pta, X, lnl, _ = load_golden(name)
+    o = oracle_for(pta, fixed=pta.white_fixed())
+    const_ = pta.constant_values()
+    for x, want in zip(X, lnl):
+        d = dict(const_)
+        d.update(pta.map_params(x))
+        got = o.lnlikelihood(d)
+        if np.isfinite(want):
+            assert abs(got - want) <= 1e-9 * abs(want)
+        else:
+            assert got == want
+
+
+def test_oracle_fixed_white_equals_varying():
+    """enterprise's TNT cache is an optimisation only: fixed-WN and
+    recomputed-WN routes give the same lnL."""
+    pta, X, _, _ = load_golden("c3_small")
+    a = oracle_for(pta, fixed=True)
+    b = oracle_for(pta, fixed=False)
+    const_ = pta.constant_values()
+    for x in X[:4]:
+        d = dict(const_)
+        d.update(pta.map_params(x))
+        la, lb = a.lnlikelihood(d), b.lnlikelihood(d)
+        assert abs(la - lb) <= 1e-9 * abs(la)
