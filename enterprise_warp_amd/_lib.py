@@ -56,6 +56,14 @@ def load():
     global _lib
     if _lib is not None:
         return _lib
+    # The HIP runtime must be loaded once per process.  torch ships its own
+    # libamdhip64 (same SONAME as /opt/rocm's); if our library is loaded
+    # first, torch later maps a second runtime and device queries fail.  Load
+    # torch's runtime first so libewarp_hip.so binds to it.
+    try:
+        import torch  # noqa: F401
+    except Exception:  # noqa: BLE001 - torch is optional for the ABI itself
+        pass
     if not os.path.exists(LIB_PATH):
         raise EngineError(f"{LIB_PATH} not built: run `make -C enterprise_warp_amd/csrc` or "
                           "__graft_entry__.build(); there is no CPU fallback")

@@ -61,30 +61,93 @@ __device__ __forceinline__ double pref_val(const ewh_pref& r, const double* th) 
   return r.idx >= 0 ? th[r.idx] : r.cval;
 }
 
-// phi of one spectral entry; restates [ent] utils.powerlaw, the reference's
-// powerlaw_bpl (enterprise_models.py:553-563) and [ent] gp_priors.free_spectrum
-// with the same operation order.
-__device__ double spec_phi(const ewh_spec_entry& s, const double* th) {
+// Device form of one spectral entry (built from ewh_spec_entry at create).
+// phi is evaluated as one exp of a sum of logs:
+//   POWERLAW  A^2/(12 pi^2) fyr^(g-3) f^-g df = exp(a + 2 ln10 lgA + (g-3) ln fyr - g ln f)
+//   TURNOVER  A^2/(12 pi^2) fyr^-3 ((f+fc)/fyr)^-g df
+//             = exp(a + 2 ln10 lgA - 3 ln fyr - g (ln(f+fc) - ln fyr)),  fc = 10^fc if fc < 0
+//   FREESPEC  10^(2 rho) = exp(2 ln10 rho)
+//   CONST     v0
+// with a = ln(df / (12 pi^2)); the same quantities as [ent] utils.powerlaw,
+// the reference's powerlaw_bpl (enterprise_models.py:553-563) and
+// [ent] gp_priors.free_spectrum, re-associated (relative error ~1e-14).
+struct DSpec {
+  int kind, col;
+  int i0, i1, i2, pad_;
+  double v0, v1, v2;     // constant values of the three parameters
+  double a, lnf, lnfyr, f;
+};
+
+__device__ __forceinline__ double dpar(int idx, double cval, const double* th) {
+  return idx >= 0 ? th[idx] : cval;
+}
+
+constexpr double LN10 = 2.302585092994045684;
+
+// __noinline__: ROCm 7.2 clang crashes in the CGSCC inliner when this is inlined into both
+// the schur and LDS-Cholesky kernels; it runs before the factorisation, so the call is cheap.
+__device__ __noinline__ double spec_phi(const DSpec& s, const double* th) {
   switch (s.kind) {
     case EWH_SPEC_POWERLAW: {
-      const double lgA = pref_val(s.p0, th), gam = pref_val(s.p1, th);
-      const double A = pow(10.0, lgA);
-      return A * A / 12.0 / (M_PI * M_PI) * pow(s.fyr, gam - 3.0) * pow(s.f, -gam) * s.df;
+      const double lgA = dpar(s.i0, s.v0, th), gam = dpar(s.i1, s.v1, th);
+      return exp(s.a + 2.0 * LN10 * lgA + (gam - 3.0) * s.lnfyr - gam * s.lnf);
     }
     case EWH_SPEC_TURNOVER: {
-      const double lgA = pref_val(s.p0, th), gam = pref_val(s.p1, th);
-      double fc = pref_val(s.p2, th);
-      if (fc < 0) fc = pow(10.0, fc);
-      const double A = pow(10.0, lgA);
-      return A * A / 12.0 / (M_PI * M_PI) * pow(s.fyr, -3.0) * pow((s.f + fc) / s.fyr, -gam) * s.df;
+      const double lgA = dpar(s.i0, s.v0, th), gam = dpar(s.i1, s.v1, th);
+      double fc = dpar(s.i2, s.v2, th);
+      if (fc < 0) fc = exp(LN10 * fc);
+      return exp(s.a + 2.0 * LN10 * lgA - 3.0 * s.lnfyr - gam * (log(s.f + fc) - s.lnfyr));
     }
     case EWH_SPEC_FREESPEC:
-      return pow(10.0, 2.0 * pref_val(s.p0, th));
+      return exp(2.0 * LN10 * dpar(s.i0, s.v0, th));
     case EWH_SPEC_CONST:
-      return s.p0.cval;
+      return s.v0;
     default:
       return __builtin_nan("");
   }
+}
+
+// running log-determinant without a log per term: product of frexp mantissas
+// (each in [0.5, 1): >= 2^-1000 after 1000 terms, no underflow) + exponent sum.
+struct LogAcc {
+  double mant = 1.0;
+  int ex = 0;
+  __device__ __forceinline__ void add(double x) {
+    mant *= __builtin_amdgcn_frexp_mant(x);   // <= 1000 terms: no renormalisation needed
+    ex += __builtin_amdgcn_frexp_exp(x);
+  }
+  __device__ __forceinline__ double value() const { return log(mant) + ex * 0.69314718055994530942; }
+};
+
+__device__ __forceinline__ double readlane_d(double x, int lane) {
+  const int lo = __builtin_amdgcn_readlane(__double2loint(x), lane);
+  const int hi = __builtin_amdgcn_readlane(__double2hiint(x), lane);
+  return __hiloint2double(hi, lo);
+}
+
+// value of lane 16*G + (lane & 15): broadcast lane group G (one row of a
+// 16x16 C/D block register) to all four groups with v_permlane32_swap +
+// v_permlane16_swap (VALU, no LDS round trip).  tests/hip/lane_ops_test.hip.
+template <int G>
+__device__ __forceinline__ double bcast_group(double x) {
+  const unsigned lo = __double2loint(x), hi = __double2hiint(x);
+  auto a = __builtin_amdgcn_permlane32_swap(lo, lo, false, false);
+  auto b = __builtin_amdgcn_permlane32_swap(hi, hi, false, false);
+  const unsigned l2 = (G < 2) ? a[0] : a[1], h2 = (G < 2) ? b[0] : b[1];
+  auto c = __builtin_amdgcn_permlane16_swap(l2, l2, false, false);
+  auto d = __builtin_amdgcn_permlane16_swap(h2, h2, false, false);
+  const unsigned l3 = (G & 1) ? c[1] : c[0], h3 = (G & 1) ? d[1] : d[0];
+  return __hiloint2double((int)h3, (int)l3);
+}
+
+// 1/sqrt(a): hardware estimate + two Newton steps (~1 ulp).
+__device__ __forceinline__ double rsqrt_nr(double a) {
+  double y = __builtin_amdgcn_rsq(a);
+  const double h = 0.5 * a;
+  double t = fma(-h * y, y, 0.5);
+  y = fma(y, t, y);
+  t = fma(-h * y, y, 0.5);
+  return fma(y, t, y);
 }
 
 __device__ __forceinline__ double wave_sum(double v) {
@@ -128,7 +191,7 @@ struct CholJob {
   int ld;                    // leading dimension (= 16 * NB)
   int mreal;                 // columns with a phi entry (0..mreal-1); r at ld-1
   const int* col_ptr;        // CSR of spectral entries over mreal columns
-  const ewh_spec_entry* spec;
+  const DSpec* spec;
   const double* K;           // additive constant, K[(b - b_off) * kstride]
   int kstride;
   int fail;                  // 1: lead block not positive definite -> -inf
@@ -272,7 +335,7 @@ __global__ __launch_bounds__(256) void contract_mfma_kernel(PsrDev P, const doub
 // ----------------------------------------------------------------------------
 __global__ __launch_bounds__(256) void schur_kernel(double* G, int ld, int m, int nlead,
                                                     const int* __restrict__ col_ptr,
-                                                    const ewh_spec_entry* __restrict__ spec,
+                                                    const DSpec* __restrict__ spec,
                                                     double Kb, double* S, int fx_ld, int fx_m,
                                                     double* Kout, int* fail_out) {
   __shared__ double row[256 * 4];
@@ -343,34 +406,34 @@ __global__ __launch_bounds__(256) void chol_lds_kernel(const CholJob* __restrict
     for (int j = lane; j <= i; j += 64) L[base + j] = A[(long long)gi * ld + (j < mr ? j : ld - 1)];
   }
   __syncthreads();
-  double lphi = 0.0;
+  LogAcc lphi;
   for (int a = threadIdx.x; a < mr; a += 256) {
     double ph = 0.0;
     for (int e = J.col_ptr[a]; e < J.col_ptr[a + 1]; ++e) ph += spec_phi(J.spec[e], th);
     L[a * (a + 1) / 2 + a] += 1.0 / ph;
-    lphi += log(ph);
+    lphi.add(ph);
   }
-  lphi = block_sum256(lphi, red);
+  const double lphi_sum = block_sum256(lphi.value(), red);
   __syncthreads();
-  double logdet = 0.0;
+  LogAcc ldet;                                  // sum of log pivots = 2 sum log U_jj
   bool ok = true;
   for (int k = 0; k < ma - 1; ++k) {
     const double piv = L[k * (k + 1) / 2 + k];
     ok = ok && (piv > 0.0);
-    const double d = sqrt(piv), rinv = 1.0 / d;
-    logdet += log(d);
+    ldet.add(piv);
+    const double rinv = rsqrt_nr(piv);
     for (int i = k + 1 + threadIdx.x; i < ma; i += 256) col[i] = L[i * (i + 1) / 2 + k] * rinv;
     __syncthreads();
     for (int i = k + 1 + wave; i < ma; i += 4) {
       const double ci = col[i];
       const int base = i * (i + 1) / 2;
-      for (int j = k + 1 + lane; j <= i; j += 64) L[base + j] -= ci * col[j];
+      for (int j = k + 1 + lane; j <= i; j += 64) L[base + j] = fma(-ci, col[j], L[base + j]);
     }
     __syncthreads();
   }
   const double qv = L[(ma - 1) * ma / 2 + ma - 1];
   if (threadIdx.x == 0) {
-    double lnl = J.K[(long long)(b - b_off) * J.kstride] - 0.5 * qv - logdet - 0.5 * lphi;
+    double lnl = J.K[(long long)(b - b_off) * J.kstride] - 0.5 * qv - 0.5 * ldet.value() - 0.5 * lphi_sum;
     if (!ok || J.fail) lnl = -INFINITY;
     out_units[(long long)p * B + b] = lnl;
   }
@@ -381,11 +444,12 @@ __global__ __launch_bounds__(256) void chol_lds_kernel(const CholJob* __restrict
 // The upper triangle of the LD x LD matrix (LD = 16 NB) lives in registers as
 // NB(NB+1)/2 16x16 blocks in the v_mfma_f64_16x16x4_f64 C/D layout
 // (lane l, reg r <-> row (l>>4) + 4r, col l&15).  Factor A = U^T U (upper,
-// as LAPACK dpotrf 'U' behind scipy cho_factor): for each block row b the
-// 16 pivots of the panel are done by VALU with cross-lane shuffles, then the
-// trailing blocks get A_ij -= U_bi^T U_bj by four MFMAs each — U_bi's
-// register s IS the MFMA A operand of k-slice s and U_bj's the B operand,
-// so the update needs no data movement at all.
+// as LAPACK dpotrf 'U' behind scipy cho_factor): for each block row bb the
+// 16 pivots of the panel are done by VALU (pivot by readlane, row k
+// broadcast by permlane swaps, only the rows that can still change are
+// touched), then the trailing blocks get A_ij -= U_bi^T U_bj by four MFMAs
+// each — U_bi's register s IS the MFMA A operand of k-slice s and U_bj's the
+// B operand, so the update needs no data movement at all.
 // ----------------------------------------------------------------------------
 template <int NB>
 struct Tri {
@@ -402,7 +466,8 @@ __device__ __forceinline__ void static_for(F&& f) {
   }
 }
 
-template <int NB>
+// BC: 0 = row broadcast by permlane swaps (VALU), 1 = by ds_bpermute (LDS crossbar)
+template <int NB, int BC>
 __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(1, 1)))
 void chol_mfma_kernel(const CholJob* __restrict__ jobs, int B, long long u0, int b_off,
                       const double* __restrict__ theta, int ldth, double* __restrict__ out_units) {
@@ -417,18 +482,18 @@ void chol_mfma_kernel(const CholJob* __restrict__ jobs, int B, long long u0, int
   const double* A = J.mats + (long long)(b - b_off) * J.mstride;
   const double* th = theta + (long long)b * ldth;
 
-  double lphi = 0.0;
+  LogAcc lphi;
   for (int a = lane; a < LD; a += 64) {
     double pi = 0.0;
     if (a < J.mreal) {
       double ph = 0.0;
       for (int e = J.col_ptr[a]; e < J.col_ptr[a + 1]; ++e) ph += spec_phi(J.spec[e], th);
       pi = 1.0 / ph;
-      lphi += log(ph);
+      lphi.add(ph);
     }
     phinv[a] = pi;
   }
-  lphi = wave_sum(lphi);
+  const double lphi_sum = wave_sum(lphi.value());
   __syncthreads();
 
   v4d U[T::n];
@@ -452,7 +517,7 @@ void chol_mfma_kernel(const CholJob* __restrict__ jobs, int B, long long u0, int
     });
   });
 
-  double logdet = 0.0;
+  LogAcc ldet;
   bool ok = true;
   static_for<0, NB>([&](auto BB) {
     constexpr int bb = decltype(BB)::value;
@@ -460,28 +525,31 @@ void chol_mfma_kernel(const CholJob* __restrict__ jobs, int B, long long u0, int
     static_for<0, (bb == NB - 1 ? 15 : 16)>([&](auto K) {
       constexpr int k = decltype(K)::value;
       constexpr int kq = k & 3, kr = k >> 2;
-      const double piv = __shfl(U[T::idx(bb, bb)][kr], 16 * kq + k);
+      const double piv = readlane_d(U[T::idx(bb, bb)][kr], 16 * kq + k);   // wave-uniform
       ok = ok && (piv > 0.0);
-      const double d = sqrt(piv), rinv = 1.0 / d;
-      logdet += log(d);
-      const bool rowk = (q == kq);
+      ldet.add(piv);
+      const double rin = rsqrt_nr(piv);                                    // wave-uniform input
+      const double sc = (q == kq) ? rin : 1.0;                             // scales row k only
+      const double xbb = U[T::idx(bb, bb)][kr] * sc;
+      // U[k][q + 4r] for this lane's rows; rows <= k are final (r < kr never
+      // changes, r == kr only for q > kq)
+      double ui[4];
+      static_for<kr, 4>([&](auto R) {
+        constexpr int r = decltype(R)::value;
+        const double v = __shfl(xbb, 16 * kq + q + 4 * r);
+        ui[r] = (r > kr || q > kq) ? v : 0.0;
+      });
       double rk[NB];
       static_for<bb, NB>([&](auto JJ) {
         constexpr int j = decltype(JJ)::value;
-        double x = U[T::idx(bb, j)][kr];
-        x = rowk ? x * rinv : x;
+        const double x = (j == bb) ? xbb : U[T::idx(bb, j)][kr] * sc;
         U[T::idx(bb, j)][kr] = x;
-        rk[j] = __shfl(x, 16 * kq + c);               // U[k][col c] of block (bb, j)
-      });
-      double ui[4];
-      static_for<0, 4>([&](auto R) {
-        constexpr int r = decltype(R)::value;
-        const double v = __shfl(U[T::idx(bb, bb)][kr], 16 * kq + q + 4 * r);  // U[k][q+4r]
-        ui[r] = (q + 4 * r > k) ? v : 0.0;
+        if constexpr (BC == 0) rk[j] = bcast_group<kq>(x);                   // U[k][col c] of block (bb, j)
+        else rk[j] = __shfl(x, 16 * kq + c);
       });
       static_for<bb, NB>([&](auto JJ) {
         constexpr int j = decltype(JJ)::value;
-        static_for<0, 4>([&](auto R) {
+        static_for<kr, 4>([&](auto R) {
           constexpr int r = decltype(R)::value;
           U[T::idx(bb, j)][r] = fma(-ui[r], rk[j], U[T::idx(bb, j)][r]);
         });
@@ -500,9 +568,9 @@ void chol_mfma_kernel(const CholJob* __restrict__ jobs, int B, long long u0, int
       });
     });
   });
-  const double qv = __shfl(U[T::idx(NB - 1, NB - 1)][3], 63);
+  const double qv = readlane_d(U[T::idx(NB - 1, NB - 1)][3], 63);
   if (lane == 0) {
-    double lnl = J.K[(long long)(b - b_off) * J.kstride] - 0.5 * qv - logdet - 0.5 * lphi;
+    double lnl = J.K[(long long)(b - b_off) * J.kstride] - 0.5 * qv - 0.5 * ldet.value() - 0.5 * lphi_sum;
     if (!ok || J.fail) lnl = -INFINITY;
     out_units[(long long)p * B + b] = lnl;
   }
@@ -528,9 +596,9 @@ struct PsrHost {
   int fx_m = 0, fx_ld = 0, fx_nb = 0;
   PsrDev dev{};
   int* d_colptr = nullptr;        // varying CSR (m+1)
-  ewh_spec_entry* d_spec = nullptr;
+  DSpec* d_spec = nullptr;
   int* d_fx_colptr = nullptr;     // fixed CSR (fx_m+1), entries re-indexed
-  ewh_spec_entry* d_fx_spec = nullptr;
+  DSpec* d_fx_spec = nullptr;
   double* d_S = nullptr;          // fx_ld^2
   bool has_theta_white = false;
 };
@@ -634,22 +702,31 @@ int validate(const ewh_pta_desc* d) {
   return 0;
 }
 
-// CSR over columns [c0, c1) re-indexed to start at 0.
-void build_csr(const ewh_pulsar_desc& s, int c0, int c1, std::vector<int>& ptr, std::vector<ewh_spec_entry>& ent) {
+DSpec to_dspec(const ewh_spec_entry& e, int col) {
+  DSpec d{};
+  d.kind = e.kind;
+  d.col = col;
+  d.i0 = e.p0.idx; d.i1 = e.p1.idx; d.i2 = e.p2.idx;
+  d.v0 = e.p0.cval; d.v1 = e.p1.cval; d.v2 = e.p2.cval;
+  d.f = e.f;
+  d.lnf = e.f > 0 ? std::log(e.f) : 0.0;
+  d.lnfyr = e.fyr > 0 ? std::log(e.fyr) : 0.0;
+  d.a = e.df > 0 ? std::log(e.df / (12.0 * M_PI * M_PI)) : 0.0;
+  return d;
+}
+
+// CSR over columns [c0, c1) re-indexed to start at 0 (caller's entry order kept per column).
+void build_csr(const ewh_pulsar_desc& s, int c0, int c1, std::vector<int>& ptr, std::vector<DSpec>& ent) {
   const int n = c1 - c0;
   ptr.assign(n + 1, 0);
   for (int e = 0; e < s.n_spec; ++e)
     if (s.spec[e].col >= c0 && s.spec[e].col < c1) ptr[s.spec[e].col - c0 + 1]++;
   for (int j = 0; j < n; ++j) ptr[j + 1] += ptr[j];
-  ent.assign(ptr[n], ewh_spec_entry{});
+  ent.assign(ptr[n], DSpec{});
   std::vector<int> fill(ptr.begin(), ptr.end() - 1);
-  for (int e = 0; e < s.n_spec; ++e) {  // keeps the caller's entry order per column
+  for (int e = 0; e < s.n_spec; ++e) {
     const int cc = s.spec[e].col;
-    if (cc >= c0 && cc < c1) {
-      ewh_spec_entry x = s.spec[e];
-      x.col = cc - c0;
-      ent[fill[cc - c0]++] = x;
-    }
+    if (cc >= c0 && cc < c1) ent[fill[cc - c0]++] = to_dspec(s.spec[e], cc - c0);
   }
 }
 
@@ -681,17 +758,21 @@ int dispatch_contract(int nb, const PsrDev& P, const double* w, const double* be
   return 0;
 }
 
-template <int NB>
+template <int NB, int BC = 0>
 void launch_chol_mfma(const CholJob* jobs, int B, long long u0, long long n, int b_off, const double* theta, int ldth,
                       double* units, hipStream_t st) {
-  hipLaunchKernelGGL(HIP_KERNEL_NAME(chol_mfma_kernel<NB>), dim3((unsigned)n), dim3(64), 0, st, jobs, B, u0, b_off,
-                     theta, ldth, units);
+  hipLaunchKernelGGL(HIP_KERNEL_NAME(chol_mfma_kernel<NB, BC>), dim3((unsigned)n), dim3(64), 0, st, jobs, B, u0,
+                     b_off, theta, ldth, units);
 }
 
 int dispatch_chol(int mode, int nb, int mreal, const CholJob* jobs, int B, long long u0, long long n, int b_off,
                   const double* theta, int ldth, double* units, hipStream_t st) {
   if (n <= 0) return 0;
-  if (mode == 0 && nb <= MFMA_NB_MAX) {
+  if (mode == 2 && nb == 8) {   // experimental: ds_bpermute row broadcast
+    launch_chol_mfma<8, 1>(jobs, B, u0, n, b_off, theta, ldth, units, st);
+    return 0;
+  }
+  if ((mode == 0 || mode == 2) && nb <= MFMA_NB_MAX) {
     switch (nb) {
       case 1: launch_chol_mfma<1>(jobs, B, u0, n, b_off, theta, ldth, units, st); return 0;
       case 2: launch_chol_mfma<2>(jobs, B, u0, n, b_off, theta, ldth, units, st); return 0;
@@ -883,7 +964,7 @@ int ewh_create(const ewh_pta_desc* d, int device, ewh_handle** out) {
     if ((rc = dupload(h, &d_eslot, s.epoch_slot, (size_t)s.n_epoch))) return bail(rc);
     ps.dev = PsrDev{s.n_toa, s.n_col, ps.ld, ps.nb, s.n_epoch, dT, dsig2, d_ef, d_eq, d_slots, d_es, d_ee, d_eslot};
     std::vector<int> ptr;
-    std::vector<ewh_spec_entry> ent;
+    std::vector<DSpec> ent;
     build_csr(s, 0, s.n_col, ptr, ent);
     if ((rc = dupload(h, &ps.d_colptr, ptr.data(), ptr.size()))) return bail(rc);
     if ((rc = dupload(h, &ps.d_spec, ent.data(), ent.size()))) return bail(rc);
@@ -902,7 +983,7 @@ int ewh_create(const ewh_pta_desc* d, int device, ewh_handle** out) {
 }
 
 int ewh_set_kernel_mode(ewh_handle* h, int32_t mode) {
-  if (!h || mode < 0 || mode > 1) return set_err(EWH_E_INVALID, "bad handle / mode");
+  if (!h || mode < 0 || mode > 2) return set_err(EWH_E_INVALID, "bad handle / mode");
   h->kernel_mode = mode;
   return 0;
 }
@@ -921,7 +1002,7 @@ int ewh_lnl_units_device(ewh_handle* h, const double* theta_dev, int32_t B, int6
   u_begin = std::max<int64_t>(0, u_begin);
   u_end = std::min<int64_t>(U, u_end);
   EWH_HIP(hipSetDevice(h->device));
-  hipStream_t st = stream ? (hipStream_t)stream : h->stream;
+  hipStream_t st = (hipStream_t)stream;   // NULL = the default stream, as documented
   int rc;
   if ((rc = ensure_units(h, B))) return rc;
   EWH_HIP(hipMemsetAsync(h->d_units, 0, sizeof(double) * (size_t)h->P * B, st));

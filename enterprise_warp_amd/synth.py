@@ -27,11 +27,13 @@ from .signals import TimingModel
 MJD0 = 53000.0
 
 
-def make_pulsar(name, n_toa, tspan_yr=15.0, seed=0, n_backends=4, epoch_size=16, n_tm=12,
+def make_pulsar(name, n_toa, tspan_yr=14.7, seed=0, n_backends=4, epoch_size=16, n_tm=12,
                 sigma_range_us=(0.1, 3.0), freq_range=(700.0, 3500.0), pos=None):
     """Synthetic pulsar: epochs of `epoch_size` TOAs (channels) from one
     backend, within 0.15 s of each other (one ECORR epoch each), spread
-    uniformly over `tspan_yr`; log-uniform radio frequencies and TOA errors;
+    uniformly over `tspan_yr` (default 14.7 yr: an integer number of years
+    would put Fourier mode Tspan/yr exactly on the yearly astrometric
+    timing-model column and make Sigma singular for loud red noise); log-uniform radio frequencies and TOA errors;
     an n_tm-column linear timing model; residuals zero (see simulate)."""
     rng = np.random.default_rng(seed)
     n_ep = max(1, n_toa // epoch_size)
@@ -228,7 +230,7 @@ def near_draws(pta, values, B, seed, scale=0.3):
 # ----------------------------------------------------------------------------
 def config_c2(seed=2, n_toa=10000, fixed_white=False, epoch_size=16):
     psr = make_pulsar("J0000+0002", n_toa, seed=seed, epoch_size=epoch_size)
-    ns = params_namespace(15.0 * const.yr, fixed_white)
+    ns = params_namespace(psr.toas.max() - psr.toas.min(), fixed_white)
     wn = white_noisedict([psr], seed + 1)
     terms = {"efac": "by_backend", "equad": "by_backend", "ecorr": "by_backend",
              "spin_noise": "powerlaw_30_nfreqs", "dm_noise": "powerlaw_30_nfreqs"}

@@ -19,8 +19,11 @@ run() {  # run <name> <seconds> cmd...
   if crash $rc; then echo "crash-class exit $rc in $name: stopping"; exit $rc; fi
   return 0
 }
+run lane_ops 120 bash -c "hipcc --offload-arch=gfx950 -O2 -o /tmp/lane_ops_test tests/hip/lane_ops_test.hip && /tmp/lane_ops_test"
 run smoke 400 python __graft_entry__.py smoke
 run pytest_gpu 900 python -m pytest tests -q -m gpu -x
 run bench 600 python bench.py --steps 10 --warmup 2
+run chol_ab 600 python scripts/chol_ab.py --rounds 5
+rocprofv3 -L > gpurun_out/counters_list.txt 2>&1 || true
 run rocprof 600 rocprofv3 --kernel-trace --stats -d gpurun_out/prof_$TAG -o run --output-format csv -- python bench.py --steps 5 --warmup 1 --no-cpu-baseline
 echo ALL_DONE

@@ -11,8 +11,12 @@ pytestmark = pytest.mark.gpu
 
 
 def _check(got, want, min_eig, label):
+    """Finite oracle values must match within the tolerance; on the Cholesky
+    failure boundary (|lambda_min| of the scaled Sigma < 1e-10) either side
+    may legitimately be -inf (SURVEY.md §7 'Hard parts')."""
     want = np.asarray(want)
-    fin = np.isfinite(want)
+    boundary = (np.abs(min_eig) < 1e-10) if min_eig is not None else np.zeros(len(want), bool)
+    fin = np.isfinite(want) & ~(boundary & ~np.isfinite(got))
     tol = lnl_tolerance(want[fin], min_eig[fin] if min_eig is not None else None)
     err = np.abs(got[fin] - want[fin])
     bad = err > tol
@@ -20,9 +24,8 @@ def _check(got, want, min_eig, label):
                           f"(tol {tol[np.argmax(err)]:.3e})"
     # -inf pattern: every oracle failure must be a failure here too unless the
     # sample sits on the failure boundary (numerically singular Sigma)
-    if min_eig is not None:
-        robust = ~fin & (np.abs(min_eig) > 1e-10)
-        assert np.all(~np.isfinite(got[robust])), f"{label}: -inf pattern differs"
+    robust = ~np.isfinite(want) & ~boundary
+    assert np.all(~np.isfinite(got[robust])), f"{label}: -inf pattern differs"
 
 
 @pytest.mark.parametrize("name", GOLDEN_NAMES)
