@@ -125,21 +125,6 @@ __device__ __forceinline__ double readlane_d(double x, int lane) {
   return __hiloint2double(hi, lo);
 }
 
-// value of lane 16*G + (lane & 15): broadcast lane group G (one row of a
-// 16x16 C/D block register) to all four groups with v_permlane32_swap +
-// v_permlane16_swap (VALU, no LDS round trip).  tests/hip/lane_ops_test.hip.
-template <int G>
-__device__ __forceinline__ double bcast_group(double x) {
-  const unsigned lo = __double2loint(x), hi = __double2hiint(x);
-  auto a = __builtin_amdgcn_permlane32_swap(lo, lo, false, false);
-  auto b = __builtin_amdgcn_permlane32_swap(hi, hi, false, false);
-  const unsigned l2 = (G < 2) ? a[0] : a[1], h2 = (G < 2) ? b[0] : b[1];
-  auto c = __builtin_amdgcn_permlane16_swap(l2, l2, false, false);
-  auto d = __builtin_amdgcn_permlane16_swap(h2, h2, false, false);
-  const unsigned l3 = (G & 1) ? c[1] : c[0], h3 = (G & 1) ? d[1] : d[0];
-  return __hiloint2double((int)h3, (int)l3);
-}
-
 // 1/sqrt(a): hardware estimate + two Newton steps (~1 ulp).
 __device__ __forceinline__ double rsqrt_nr(double a) {
   double y = __builtin_amdgcn_rsq(a);
@@ -446,7 +431,7 @@ __global__ __launch_bounds__(256) void chol_lds_kernel(const CholJob* __restrict
 // (lane l, reg r <-> row (l>>4) + 4r, col l&15).  Factor A = U^T U (upper,
 // as LAPACK dpotrf 'U' behind scipy cho_factor): for each block row bb the
 // 16 pivots of the panel are done by VALU (pivot by readlane, row k
-// broadcast by permlane swaps, only the rows that can still change are
+// broadcast by ds_bpermute, only the rows that can still change are
 // touched), then the trailing blocks get A_ij -= U_bi^T U_bj by four MFMAs
 // each — U_bi's register s IS the MFMA A operand of k-slice s and U_bj's the
 // B operand, so the update needs no data movement at all.
@@ -466,8 +451,9 @@ __device__ __forceinline__ void static_for(F&& f) {
   }
 }
 
-// BC: 0 = row broadcast by permlane swaps (VALU), 1 = by ds_bpermute (LDS crossbar)
-template <int NB, int BC>
+// FULL: 1 = every panel step unrolled (large code), 0 = runtime loop over the
+// row's lane group (the default; faster on MI355X)
+template <int NB, int FULL>
 __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(1, 1)))
 void chol_mfma_kernel(const CholJob* __restrict__ jobs, int B, long long u0, int b_off,
                       const double* __restrict__ theta, int ldth, double* __restrict__ out_units) {
@@ -521,39 +507,50 @@ void chol_mfma_kernel(const CholJob* __restrict__ jobs, int B, long long u0, int
   bool ok = true;
   static_for<0, NB>([&](auto BB) {
     constexpr int bb = decltype(BB)::value;
-    // panel row bb: 16 pivots by VALU (the r column, last of all, is not pivoted)
-    static_for<0, (bb == NB - 1 ? 15 : 16)>([&](auto K) {
-      constexpr int k = decltype(K)::value;
-      constexpr int kq = k & 3, kr = k >> 2;
-      const double piv = readlane_d(U[T::idx(bb, bb)][kr], 16 * kq + k);   // wave-uniform
-      ok = ok && (piv > 0.0);
-      ldet.add(piv);
-      const double rin = rsqrt_nr(piv);                                    // wave-uniform input
-      const double sc = (q == kq) ? rin : 1.0;                             // scales row k only
-      const double xbb = U[T::idx(bb, bb)][kr] * sc;
-      // U[k][q + 4r] for this lane's rows; rows <= k are final (r < kr never
-      // changes, r == kr only for q > kq)
-      double ui[4];
-      static_for<kr, 4>([&](auto R) {
-        constexpr int r = decltype(R)::value;
-        const double v = __shfl(xbb, 16 * kq + q + 4 * r);
-        ui[r] = (r > kr || q > kq) ? v : 0.0;
-      });
-      double rk[NB];
-      static_for<bb, NB>([&](auto JJ) {
-        constexpr int j = decltype(JJ)::value;
-        const double x = (j == bb) ? xbb : U[T::idx(bb, j)][kr] * sc;
-        U[T::idx(bb, j)][kr] = x;
-        if constexpr (BC == 0) rk[j] = bcast_group<kq>(x);                   // U[k][col c] of block (bb, j)
-        else rk[j] = __shfl(x, 16 * kq + c);
-      });
-      static_for<bb, NB>([&](auto JJ) {
-        constexpr int j = decltype(JJ)::value;
+    // panel row bb: 16 pivots by VALU (the r column, last of all, is not pivoted).
+    // Register / block indices are compile-time (kr, j, r); the row's lane
+    // group kq is a runtime loop unless FULL, which keeps the code ~4x smaller
+    // (instruction-cache resident with four waves per CU).
+    static_for<0, 4>([&](auto KR) {
+      constexpr int kr = decltype(KR)::value;
+      auto step = [&](const int kq) {
+        const int k = 4 * kr + kq;
+        const double piv = readlane_d(U[T::idx(bb, bb)][kr], 16 * kq + k);   // wave-uniform
+        ok = ok && (piv > 0.0);
+        ldet.add(piv);
+        const double rin = rsqrt_nr(piv);
+        const double sc = (q == kq) ? rin : 1.0;                             // scales row k only
+        const double xbb = U[T::idx(bb, bb)][kr] * sc;
+        // U[k][q + 4r] for this lane's rows; rows <= k are final (r < kr never
+        // changes, r == kr only for q > kq)
+        double ui[4];
         static_for<kr, 4>([&](auto R) {
           constexpr int r = decltype(R)::value;
-          U[T::idx(bb, j)][r] = fma(-ui[r], rk[j], U[T::idx(bb, j)][r]);
+          const double v = __shfl(xbb, 16 * kq + q + 4 * r);
+          ui[r] = (r > kr || q > kq) ? v : 0.0;
         });
-      });
+        double rk[NB];
+        static_for<bb, NB>([&](auto JJ) {
+          constexpr int j = decltype(JJ)::value;
+          const double x = (j == bb) ? xbb : U[T::idx(bb, j)][kr] * sc;
+          U[T::idx(bb, j)][kr] = x;
+          rk[j] = __shfl(x, 16 * kq + c);                                    // U[k][col c] of block (bb, j)
+        });
+        static_for<bb, NB>([&](auto JJ) {
+          constexpr int j = decltype(JJ)::value;
+          static_for<kr, 4>([&](auto R) {
+            constexpr int r = decltype(R)::value;
+            U[T::idx(bb, j)][r] = fma(-ui[r], rk[j], U[T::idx(bb, j)][r]);
+          });
+        });
+      };
+      constexpr int nk = (bb == NB - 1 && kr == 3) ? 3 : 4;
+      if constexpr (FULL) {
+        static_for<0, nk>([&](auto KQ) { step(decltype(KQ)::value); });
+      } else {
+#pragma unroll 1
+        for (int kq = 0; kq < nk; ++kq) step(kq);
+      }
     });
     // trailing update A_ij -= U_bi^T U_bj, four f64 MFMAs per block
     static_for<bb + 1, NB>([&](auto II) {
@@ -758,17 +755,17 @@ int dispatch_contract(int nb, const PsrDev& P, const double* w, const double* be
   return 0;
 }
 
-template <int NB, int BC = 0>
+template <int NB, int FULL = 0>
 void launch_chol_mfma(const CholJob* jobs, int B, long long u0, long long n, int b_off, const double* theta, int ldth,
                       double* units, hipStream_t st) {
-  hipLaunchKernelGGL(HIP_KERNEL_NAME(chol_mfma_kernel<NB, BC>), dim3((unsigned)n), dim3(64), 0, st, jobs, B, u0,
+  hipLaunchKernelGGL(HIP_KERNEL_NAME(chol_mfma_kernel<NB, FULL>), dim3((unsigned)n), dim3(64), 0, st, jobs, B, u0,
                      b_off, theta, ldth, units);
 }
 
 int dispatch_chol(int mode, int nb, int mreal, const CholJob* jobs, int B, long long u0, long long n, int b_off,
                   const double* theta, int ldth, double* units, hipStream_t st) {
   if (n <= 0) return 0;
-  if (mode == 2 && nb == 8) {   // experimental: ds_bpermute row broadcast
+  if (mode == 2 && nb == 8) {   // A/B: fully unrolled panel steps
     launch_chol_mfma<8, 1>(jobs, B, u0, n, b_off, theta, ldth, units, st);
     return 0;
   }
