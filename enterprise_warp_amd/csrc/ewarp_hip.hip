@@ -426,20 +426,30 @@ __global__ __launch_bounds__(256) void chol_lds_kernel(const CholJob* __restrict
 
 // ----------------------------------------------------------------------------
 // batched Cholesky, MFMA register-blocked: one wave (64 lanes) per unit.
-// The upper triangle of the LD x LD matrix (LD = 16 NB) lives in registers as
-// NB(NB+1)/2 16x16 blocks in the v_mfma_f64_16x16x4_f64 C/D layout
-// (lane l, reg r <-> row (l>>4) + 4r, col l&15).  Factor A = U^T U (upper,
-// as LAPACK dpotrf 'U' behind scipy cho_factor): for each block row bb the
-// 16 pivots of the panel are done by VALU (pivot by readlane, row k
+// The upper triangle of the LD x LD matrix (LD = 16 NB) is held as 16x16
+// blocks in the v_mfma_f64_16x16x4_f64 C/D layout (lane l, reg r <-> row
+// (l>>4) + 4r, col l&15).  Factor A = U^T U (upper, as LAPACK dpotrf 'U'
+// behind scipy cho_factor).  Per block row bb the 16 pivots of the panel are
+// done by VALU (pivot by readlane, 1/sqrt by v_rsq_f64 + Newton, row k
 // broadcast by ds_bpermute, only the rows that can still change are
-// touched), then the trailing blocks get A_ij -= U_bi^T U_bj by four MFMAs
-// each — U_bi's register s IS the MFMA A operand of k-slice s and U_bj's the
-// B operand, so the update needs no data movement at all.
+// touched); trailing blocks get A_ij -= U_bi^T U_bj by four MFMAs each with
+// no data movement — register s of a C/D-layout block IS the MFMA A / B
+// operand of k-slice s.
+//
+// Three phases keep at most 26 blocks live for NB = 8 (36 in a plain
+// right-looking order): (1) factor block rows 0..H-1 (H = NB/2) with the
+// trailing update restricted to those rows; (2) load the trailing A22
+// triangle and apply the H panel rows to it; (3) factor A22.  Same
+// arithmetic, re-ordered (left-looking at the 2x2 block level).
 // ----------------------------------------------------------------------------
 template <int NB>
-struct Tri {
-  static constexpr int n = NB * (NB + 1) / 2;
-  static constexpr int idx(int i, int j) { return i * NB - (i * (i - 1)) / 2 + (j - i); }
+struct Split {
+  static constexpr int H = NB / 2;                    // block rows of phase 1
+  static constexpr int M = NB - H;                    // A22 block order
+  static constexpr int n1 = H * NB - H * (H - 1) / 2; // blocks (i < H, j >= i)
+  static constexpr int n2 = M * (M + 1) / 2;          // blocks (H <= i <= j)
+  static constexpr int i1(int i, int j) { return i * NB - (i * (i - 1)) / 2 + (j - i); }
+  static constexpr int i2(int i, int j) { return (i - H) * M - ((i - H) * (i - H - 1)) / 2 + (j - i); }
 };
 
 // compile-time loop: f(std::integral_constant<int, I>) for I in [B, E)
@@ -451,14 +461,24 @@ __device__ __forceinline__ void static_for(F&& f) {
   }
 }
 
+// A -= U_i^T U_j : four f64 MFMAs (A operand = -U_i)
+__device__ __forceinline__ void syrk_update(v4d& C, const v4d& Ui, const v4d& Uj) {
+#pragma unroll
+  for (int sk = 0; sk < 4; ++sk) C = __builtin_amdgcn_mfma_f64_16x16x4f64(-Ui[sk], Uj[sk], C, 0, 0, 0);
+}
+
 // FULL: 1 = every panel step unrolled (large code), 0 = runtime loop over the
-// row's lane group (the default; faster on MI355X)
-template <int NB, int FULL>
-__global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(1, 1)))
+// row's lane group (the default)
+// W: waves per SIMD the register budget is cut for (2 -> 256 VGPRs: the NB = 8
+// three-phase kernel fits with no spills, so two units share each SIMD and one's
+// MFMAs overlap the other's VALU / LDS latency).
+template <int NB, int FULL, int W>
+__global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(W, W)))
 void chol_mfma_kernel(const CholJob* __restrict__ jobs, int B, long long u0, int b_off,
                       const double* __restrict__ theta, int ldth, double* __restrict__ out_units) {
   constexpr int LD = 16 * NB;
-  using T = Tri<NB>;
+  using S = Split<NB>;
+  constexpr int H = S::H;
   __shared__ double phinv[LD];
   const int lane = threadIdx.x;
   const int q = lane >> 4, c = lane & 15;
@@ -482,45 +502,36 @@ void chol_mfma_kernel(const CholJob* __restrict__ jobs, int B, long long u0, int
   const double lphi_sum = wave_sum(lphi.value());
   __syncthreads();
 
-  v4d U[T::n];
-  static_for<0, NB>([&](auto BI) {
-    constexpr int bi = decltype(BI)::value;
-    static_for<bi, NB>([&](auto BJ) {
-      constexpr int bj = decltype(BJ)::value;
-      v4d v;
+  auto load_block = [&](auto BI, auto BJ, v4d& v) {
+    constexpr int bi = decltype(BI)::value, bj = decltype(BJ)::value;
+    static_for<0, 4>([&](auto R) {
+      constexpr int r = decltype(R)::value;
+      v[r] = A[(long long)(16 * bi + q + 4 * r) * LD + 16 * bj + c];
+    });
+    if constexpr (bi == bj) {
+      const double pd = phinv[16 * bi + c];
       static_for<0, 4>([&](auto R) {
         constexpr int r = decltype(R)::value;
-        v[r] = A[(long long)(16 * bi + q + 4 * r) * LD + 16 * bj + c];
+        v[r] += (q + 4 * r == c) ? pd : 0.0;
       });
-      if constexpr (bi == bj) {
-        const double pd = phinv[16 * bi + c];
-        static_for<0, 4>([&](auto R) {
-          constexpr int r = decltype(R)::value;
-          v[r] += (q + 4 * r == c) ? pd : 0.0;
-        });
-      }
-      U[T::idx(bi, bj)] = v;
-    });
-  });
+    }
+  };
 
   LogAcc ldet;
   bool ok = true;
-  static_for<0, NB>([&](auto BB) {
-    constexpr int bb = decltype(BB)::value;
-    // panel row bb: 16 pivots by VALU (the r column, last of all, is not pivoted).
-    // Register / block indices are compile-time (kr, j, r); the row's lane
-    // group kq is a runtime loop unless FULL, which keeps the code ~4x smaller
-    // (instruction-cache resident with four waves per CU).
+  // panel row bb over the blocks blk(j), j = bb..NB-1
+  auto panel = [&](auto BBc, auto&& blk) {
+    constexpr int bb = decltype(BBc)::value;
     static_for<0, 4>([&](auto KR) {
       constexpr int kr = decltype(KR)::value;
       auto step = [&](const int kq) {
         const int k = 4 * kr + kq;
-        const double piv = readlane_d(U[T::idx(bb, bb)][kr], 16 * kq + k);   // wave-uniform
+        const double piv = readlane_d(blk(BBc)[kr], 16 * kq + k);           // wave-uniform
         ok = ok && (piv > 0.0);
         ldet.add(piv);
         const double rin = rsqrt_nr(piv);
         const double sc = (q == kq) ? rin : 1.0;                             // scales row k only
-        const double xbb = U[T::idx(bb, bb)][kr] * sc;
+        const double xbb = blk(BBc)[kr] * sc;
         // U[k][q + 4r] for this lane's rows; rows <= k are final (r < kr never
         // changes, r == kr only for q > kq)
         double ui[4];
@@ -532,19 +543,19 @@ void chol_mfma_kernel(const CholJob* __restrict__ jobs, int B, long long u0, int
         double rk[NB];
         static_for<bb, NB>([&](auto JJ) {
           constexpr int j = decltype(JJ)::value;
-          const double x = (j == bb) ? xbb : U[T::idx(bb, j)][kr] * sc;
-          U[T::idx(bb, j)][kr] = x;
+          const double x = (j == bb) ? xbb : blk(JJ)[kr] * sc;
+          blk(JJ)[kr] = x;
           rk[j] = __shfl(x, 16 * kq + c);                                    // U[k][col c] of block (bb, j)
         });
         static_for<bb, NB>([&](auto JJ) {
           constexpr int j = decltype(JJ)::value;
           static_for<kr, 4>([&](auto R) {
             constexpr int r = decltype(R)::value;
-            U[T::idx(bb, j)][r] = fma(-ui[r], rk[j], U[T::idx(bb, j)][r]);
+            blk(JJ)[r] = fma(-ui[r], rk[j], blk(JJ)[r]);
           });
         });
       };
-      constexpr int nk = (bb == NB - 1 && kr == 3) ? 3 : 4;
+      constexpr int nk = (bb == NB - 1 && kr == 3) ? 3 : 4;   // the r column is not pivoted
       if constexpr (FULL) {
         static_for<0, nk>([&](auto KQ) { step(decltype(KQ)::value); });
       } else {
@@ -552,20 +563,54 @@ void chol_mfma_kernel(const CholJob* __restrict__ jobs, int B, long long u0, int
         for (int kq = 0; kq < nk; ++kq) step(kq);
       }
     });
-    // trailing update A_ij -= U_bi^T U_bj, four f64 MFMAs per block
+  };
+
+  // ---- phase 1: block rows 0..H-1 ----
+  v4d U1[S::n1 > 0 ? S::n1 : 1];
+  static_for<0, H>([&](auto BI) {
+    constexpr int bi = decltype(BI)::value;
+    static_for<bi, NB>([&](auto BJ) { load_block(BI, BJ, U1[S::i1(bi, decltype(BJ)::value)]); });
+  });
+  static_for<0, H>([&](auto BBc) {
+    constexpr int bb = decltype(BBc)::value;
+    panel(BBc, [&](auto JJ) -> v4d& { return U1[S::i1(bb, decltype(JJ)::value)]; });
+    static_for<bb + 1, H>([&](auto II) {
+      constexpr int i = decltype(II)::value;
+      static_for<i, NB>([&](auto JJ) {
+        constexpr int j = decltype(JJ)::value;
+        syrk_update(U1[S::i1(i, j)], U1[S::i1(bb, i)], U1[S::i1(bb, j)]);
+      });
+    });
+  });
+  // ---- phase 2: A22 -= U12^T U12 ----
+  v4d U2[S::n2];
+  static_for<H, NB>([&](auto BI) {
+    constexpr int bi = decltype(BI)::value;
+    static_for<bi, NB>([&](auto BJ) { load_block(BI, BJ, U2[S::i2(bi, decltype(BJ)::value)]); });
+  });
+  static_for<0, H>([&](auto BBc) {
+    constexpr int bb = decltype(BBc)::value;
+    static_for<H, NB>([&](auto II) {
+      constexpr int i = decltype(II)::value;
+      static_for<i, NB>([&](auto JJ) {
+        constexpr int j = decltype(JJ)::value;
+        syrk_update(U2[S::i2(i, j)], U1[S::i1(bb, i)], U1[S::i1(bb, j)]);
+      });
+    });
+  });
+  // ---- phase 3: factor A22 ----
+  static_for<H, NB>([&](auto BBc) {
+    constexpr int bb = decltype(BBc)::value;
+    panel(BBc, [&](auto JJ) -> v4d& { return U2[S::i2(bb, decltype(JJ)::value)]; });
     static_for<bb + 1, NB>([&](auto II) {
       constexpr int i = decltype(II)::value;
       static_for<i, NB>([&](auto JJ) {
         constexpr int j = decltype(JJ)::value;
-        static_for<0, 4>([&](auto S) {
-          constexpr int sk = decltype(S)::value;
-          U[T::idx(i, j)] = __builtin_amdgcn_mfma_f64_16x16x4f64(-U[T::idx(bb, i)][sk], U[T::idx(bb, j)][sk],
-                                                                 U[T::idx(i, j)], 0, 0, 0);
-        });
+        syrk_update(U2[S::i2(i, j)], U2[S::i2(bb, i)], U2[S::i2(bb, j)]);
       });
     });
   });
-  const double qv = readlane_d(U[T::idx(NB - 1, NB - 1)][3], 63);
+  const double qv = readlane_d(U2[S::i2(NB - 1, NB - 1)][3], 63);
   if (lane == 0) {
     double lnl = J.K[(long long)(b - b_off) * J.kstride] - 0.5 * qv - 0.5 * ldet.value() - 0.5 * lphi_sum;
     if (!ok || J.fail) lnl = -INFINITY;
@@ -755,10 +800,12 @@ int dispatch_contract(int nb, const PsrDev& P, const double* w, const double* be
   return 0;
 }
 
-template <int NB, int FULL = 0>
+constexpr int default_waves(int nb) { return nb <= 8 ? 2 : 1; }
+
+template <int NB, int FULL = 0, int W = default_waves(NB)>
 void launch_chol_mfma(const CholJob* jobs, int B, long long u0, long long n, int b_off, const double* theta, int ldth,
                       double* units, hipStream_t st) {
-  hipLaunchKernelGGL(HIP_KERNEL_NAME(chol_mfma_kernel<NB, FULL>), dim3((unsigned)n), dim3(64), 0, st, jobs, B, u0,
+  hipLaunchKernelGGL(HIP_KERNEL_NAME(chol_mfma_kernel<NB, FULL, W>), dim3((unsigned)n), dim3(64), 0, st, jobs, B, u0,
                      b_off, theta, ldth, units);
 }
 
@@ -769,7 +816,11 @@ int dispatch_chol(int mode, int nb, int mreal, const CholJob* jobs, int B, long 
     launch_chol_mfma<8, 1>(jobs, B, u0, n, b_off, theta, ldth, units, st);
     return 0;
   }
-  if ((mode == 0 || mode == 2) && nb <= MFMA_NB_MAX) {
+  if (mode == 3 && nb == 8) {   // A/B: one wave per SIMD (512-register budget)
+    launch_chol_mfma<8, 0, 1>(jobs, B, u0, n, b_off, theta, ldth, units, st);
+    return 0;
+  }
+  if (mode != 1 && nb <= MFMA_NB_MAX) {
     switch (nb) {
       case 1: launch_chol_mfma<1>(jobs, B, u0, n, b_off, theta, ldth, units, st); return 0;
       case 2: launch_chol_mfma<2>(jobs, B, u0, n, b_off, theta, ldth, units, st); return 0;
@@ -980,7 +1031,7 @@ int ewh_create(const ewh_pta_desc* d, int device, ewh_handle** out) {
 }
 
 int ewh_set_kernel_mode(ewh_handle* h, int32_t mode) {
-  if (!h || mode < 0 || mode > 2) return set_err(EWH_E_INVALID, "bad handle / mode");
+  if (!h || mode < 0 || mode > 3) return set_err(EWH_E_INVALID, "bad handle / mode");
   h->kernel_mode = mode;
   return 0;
 }

@@ -144,7 +144,8 @@ double ewh_unit_cost(const ewh_handle* h, int32_t pulsar);
 
 /* Kernel selection: 0 = auto (MFMA register-blocked Cholesky when the
  * reduced matrix fits, LDS kernel otherwise), 1 = force the LDS kernel,
- * 2 = MFMA kernel with fully unrolled panel steps (A/B experiments). */
+ * 2 = MFMA kernel with fully unrolled panel steps, 3 = MFMA kernel at one
+ * wave per SIMD (A/B experiments; NB = 8 only, else as 0). */
 int ewh_set_kernel_mode(ewh_handle* h, int32_t mode);
 
 void ewh_destroy(ewh_handle* h);

@@ -6,7 +6,7 @@ cd "${GRAFT_REPO_ROOT:-/root/repo}"
 mkdir -p gpurun_out
 export TMPDIR=/tmp
 TAG=${1:-r01}
-ARGS=${2:---rounds 2 --modes 0,2}
+ARGS=${2:---rounds 2 --modes 0,3}
 crash() { case "$1" in 0|1|2|5) return 1;; *) return 0;; esac; }
 pass() {  # pass <name> counters...
   local name=$1; shift

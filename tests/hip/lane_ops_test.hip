@@ -38,6 +38,16 @@ __global__ void k_mfma(double* out) {
   for (int r = 0; r < 4; ++r) out[((l >> 4) + 4 * r) * 16 + (l & 15)] = acc[r];   // C/D: row (l>>4)+4r, col l&15
 }
 
+// f64 MFMA with BLGP = 1: negate A (CDNA f64 MFMA reuses BLGP as neg flags)
+__global__ void k_mfma_neg(double* out) {
+  const int l = threadIdx.x;
+  const int i = l & 15, kk = l >> 4;
+  const double a = i * 4 + kk + 1, b = 100.0 * kk + i + 7;
+  v4d acc = {1, 2, 3, 4};
+  acc = __builtin_amdgcn_mfma_f64_16x16x4f64(a, b, acc, 0, 0, 1);
+  for (int r = 0; r < 4; ++r) out[((l >> 4) + 4 * r) * 16 + (l & 15)] = acc[r];
+}
+
 int main() {
   double *d, h[256];
   if (hipMalloc(&d, 256 * sizeof(double)) != hipSuccess) return 2;
@@ -59,6 +69,17 @@ int main() {
         if (bad++ < 16) printf("mfma D[%d][%d] = %g want %g\n", i, j, h[i * 16 + j], want);
       }
     }
+  hipLaunchKernelGGL(k_mfma_neg, dim3(1), dim3(64), 0, 0, d);
+  hipMemcpy(h, d, 256 * sizeof(double), hipMemcpyDeviceToHost);
+  int negbad = 0;
+  for (int i = 0; i < 16; ++i)
+    for (int j = 0; j < 16; ++j) {
+      double want = 0;
+      for (int k = 0; k < 4; ++k) want += (i * 4 + k + 1) * (100.0 * k + j + 7);
+      const double init = 1.0 + ((i >> 2) & 3);   // acc[r] = r + 1 for row (l>>4) + 4r
+      if (h[i * 16 + j] != init - want) negbad++;
+    }
+  printf(negbad ? "BLGP1_NEGATES_A: no (%d mismatches)\n" : "BLGP1_NEGATES_A: yes\n", negbad);
   hipFree(d);
   if (bad) { printf("LANE_OPS_FAIL %d\n", bad); return 1; }
   printf("LANE_OPS_OK\n");
