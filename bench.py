@@ -35,26 +35,45 @@ def algorithmic_flops_per_unit(m):
     return m ** 3 / 3.0 + 2.0 * m ** 2
 
 
-def cpu_baseline(cfg, seconds):
-    """The oracle (numpy/scipy restatement of enterprise's likelihood, TNT
-    cached as enterprise caches it for fixed white noise) on one host core."""
+def _cpu_worker(args):
+    """One single-threaded process timing the oracle on C3 (spawned before
+    the parent touches the GPU)."""
+    seconds, seed = args
+    import os as _os
+    _os.environ["OMP_NUM_THREADS"] = "1"
     from threadpoolctl import threadpool_limits
+    from enterprise_warp_amd import synth
     from oracle.enterprise_ref import OraclePTA
-    pta = cfg.pta
-    const = pta.constant_values()
     with threadpool_limits(limits=1):
+        cfg = synth.config_c3()
+        pta = cfg.pta
+        const = pta.constant_values()
         o = OraclePTA([c.psr for c in pta.signal_collections], pta.oracle_terms(), fixed_params=const)
-        X = __import__("enterprise_warp_amd.synth", fromlist=["x"]).prior_draws(pta, 4096, 7)
+        X = synth.prior_draws(pta, 512, seed)
         n, t0 = 0, time.perf_counter()
         while time.perf_counter() - t0 < seconds:
             d = dict(const)
             d.update(pta.map_params(X[n % len(X)]))
             o.lnlikelihood(d)
             n += 1
-        dt = time.perf_counter() - t0
-    return {"value": n / dt, "unit": "lnL evals/s", "cores": 1, "kind": "port",
-            "sample": f"{n} evaluations of the full 45-pulsar C3 likelihood in {dt:.1f} s "
-                      "(oracle/enterprise_ref.py, cached TNT, BLAS limited to 1 thread)"}
+        return n, time.perf_counter() - t0
+
+
+def cpu_baseline(seconds, procs):
+    """The oracle (numpy/scipy restatement of enterprise's likelihood, TNT
+    cached as enterprise caches it for fixed white noise), `procs` single-
+    threaded processes evaluating independent proposals (SURVEY.md §8(d) mode
+    (ii)); aggregate evals/s."""
+    import multiprocessing as mp
+    ctx = mp.get_context("spawn")
+    with ctx.Pool(procs) as pool:
+        res = pool.map(_cpu_worker, [(seconds, 100 + i) for i in range(procs)])
+    total = sum(n / dt for n, dt in res)
+    per = [n / dt for n, dt in res]
+    return {"value": total, "unit": "lnL evals/s", "cores": procs, "kind": "port",
+            "sample": f"{procs} single-threaded processes x {seconds:.0f} s of full 45-pulsar C3 evaluations "
+                      f"(oracle/enterprise_ref.py, cached TNT); {sum(n for n, _ in res)} evaluations, "
+                      f"per-process {np.mean(per):.1f} evals/s"}
 
 
 def main():
@@ -63,7 +82,8 @@ def main():
     ap.add_argument("--steps", type=int, default=20)
     ap.add_argument("--warmup", type=int, default=3)
     ap.add_argument("--batch-per-gpu", type=int, default=4096)
-    ap.add_argument("--cpu-seconds", type=float, default=15.0)
+    ap.add_argument("--cpu-seconds", type=float, default=12.0)
+    ap.add_argument("--cpu-procs", type=int, default=min(16, len(os.sched_getaffinity(0))))
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--kernel-mode", type=int, default=0, help="0 auto (MFMA), 1 LDS fallback")
     args = ap.parse_args()
@@ -75,6 +95,11 @@ def main():
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
+    # CPU baseline first: worker processes are spawned before this process
+    # initialises the GPU (no forked child ever carries a HIP context)
+    cpu = None
+    if world == 1 and not args.no_cpu_baseline:
+        cpu = cpu_baseline(args.cpu_seconds, args.cpu_procs)
     if world > 1:
         torch.cuda.set_device(local)
         dist.init_process_group("nccl", device_id=torch.device("cuda", local))
@@ -156,8 +181,8 @@ def main():
                          "kernel": "chol_mfma_kernel<8>", "launch_ms": launch_ms,
                          "flops_per_launch": flops},
         }
-        if world == 1 and not args.no_cpu_baseline:
-            rec["cpu_baseline"] = cpu_baseline(cfg, args.cpu_seconds)
+        if cpu is not None:
+            rec["cpu_baseline"] = cpu
         print(json.dumps(rec), flush=True)
     if world > 1:
         dist.destroy_process_group()
