@@ -24,6 +24,7 @@ run smoke 400 python __graft_entry__.py smoke
 run pytest_gpu 900 python -m pytest tests -q -m gpu -x
 run bench 600 python bench.py --steps 10 --warmup 2
 run chol_ab 600 python scripts/chol_ab.py --rounds 5 --modes 0,3,2
+run configs 900 python scripts/bench_configs.py
 run pmc 1500 bash scripts/gpu_pmc.sh $TAG
 run rocprof 600 rocprofv3 --kernel-trace --stats -d gpurun_out/prof_$TAG -o run --output-format csv -- python bench.py --steps 5 --warmup 1 --no-cpu-baseline
 echo ALL_DONE
