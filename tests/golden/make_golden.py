@@ -97,6 +97,29 @@ def main():
     c3 = synth.config_c3(n_psr=4, n_min=600, n_max=1500, epoch_size=4)
     X = np.vstack([synth.prior_draws(c3.pta, 8, 31), synth.near_draws(c3.pta, c3.truth, 8, 32)])
     dump("c3_small", c3.pta, recipe_of(c3, terms_ecorr, {"gwb": "vary_gamma_14_nfreqs"}, True), X)
+    # c1 turnover: the reference's default_noise_example_2.json model for
+    # J1832-0836 (efac by backend, spin_noise turnover, dm_noise powerlaw)
+    c1t = synth.config_c1(os.path.join(HERE, "ref_examples"))
+    psr = c1t.pta.signal_collections[0].psr
+    ns = synth.params_namespace(np.ptp(psr.toas), False)
+    terms_t = {"efac": "by_backend", "spin_noise": "turnover", "dm_noise": "powerlaw"}
+    pta_t = synth.build_pta([psr], terms_t, {}, ns, None)
+    truth_t = synth.truth_values(pta_t, 5)
+    X = np.vstack([synth.prior_draws(pta_t, 8, 13), synth.near_draws(pta_t, truth_t, 8, 14)])
+    dump("c1_turnover", pta_t, {"per_psr_terms": terms_t, "common_terms": {}, "Tspan": float(np.ptp(psr.toas)),
+                                "fixed_white": False, "noisedict": {}}, X)
+    # c3 free spectrum: fixed white noise, CURN as a 10-bin free spectrum
+    c3f = synth.config_c3(n_psr=3, n_min=700, n_max=1400, epoch_size=4)
+    psrs = [c.psr for c in c3f.pta.signal_collections]
+    Tspan = max(p.toas.max() for p in psrs) - min(p.toas.min() for p in psrs)
+    ns = synth.params_namespace(Tspan, True)
+    wn = {k: v for k, v in c3f.pta.constant_values().items() if v is not None}
+    common_f = {"gwb": "freesp_10_nfreqs"}
+    pta_f = synth.build_pta(psrs, terms_ecorr, common_f, ns, wn)
+    truth_f = synth.truth_values(pta_f, 6, white=wn)
+    X = np.vstack([synth.prior_draws(pta_f, 8, 15), synth.near_draws(pta_f, truth_f, 8, 16)])
+    dump("c3_freesp", pta_f, {"per_psr_terms": terms_ecorr, "common_terms": common_f, "Tspan": float(Tspan),
+                              "fixed_white": True, "noisedict": wn}, X)
     # c4 small: varying white noise, band noise, wide basis (LDS kernel)
     c4 = synth.config_c4(n_psr=3, n_min=700, n_max=1200, epoch_size=4)
     X = np.vstack([synth.prior_draws(c4.pta, 8, 41), synth.near_draws(c4.pta, c4.truth, 8, 42)])
