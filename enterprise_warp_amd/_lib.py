@@ -10,7 +10,7 @@ import os
 _HERE = os.path.dirname(os.path.abspath(__file__))
 LIB_PATH = os.path.join(_HERE, "libewarp_hip.so")
 
-EWH_ABI_VERSION = 1
+EWH_ABI_VERSION = 2
 SPEC_POWERLAW, SPEC_TURNOVER, SPEC_FREESPEC, SPEC_CONST = 1, 2, 3, 4
 
 
@@ -33,7 +33,8 @@ class PulsarDesc(C.Structure):
                 ("n_slot", C.c_int32), ("slots", C.POINTER(Pref)),
                 ("efac_slot", _ip), ("equad_slot", _ip),
                 ("n_epoch", C.c_int32), ("epoch_start", _ip), ("epoch_stop", _ip), ("epoch_slot", _ip),
-                ("spec", C.POINTER(SpecEntry))]
+                ("spec", C.POINTER(SpecEntry)),
+                ("n_bgroup", C.c_int32), ("bgroup_idx", C.POINTER(Pref)), ("col_bgroup", _ip), ("ln_chrom", _dp)]
 
 
 class PtaDesc(C.Structure):

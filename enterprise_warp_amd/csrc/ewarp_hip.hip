@@ -167,6 +167,10 @@ struct PsrDev {
   const int* ep_start;
   const int* ep_stop;
   const int* ep_slot;
+  int n_bgroup;              // theta-dependent chromatic basis groups (0: none)
+  const int* col_bgroup;     // ld entries, -1 = fixed column
+  const double* ln_chrom;    // n_toa: ln(1400 / nu)
+  const ewh_pref* bgroup;    // n_bgroup: chromatic index per group
 };
 
 // One factorisation job: (pulsar, sample) -> matrix + diagonal update.
@@ -189,11 +193,17 @@ struct CholJob {
 __global__ __launch_bounds__(256) void wn_weights_kernel(PsrDev P, const double* __restrict__ theta,
                                                          int ldth, int b0, double* __restrict__ w,
                                                          double* __restrict__ beta,
-                                                         double* __restrict__ Kb) {
+                                                         double* __restrict__ Kb, double* __restrict__ fac) {
   __shared__ double red[4];
   const int bl = blockIdx.x;
   const double* th = theta + (long long)(b0 + bl) * ldth;
   double* wr = w + (long long)bl * P.n_toa;
+  // theta-dependent chromatic basis: fac[t][g] = (1400/nu_t)^idx_g
+  for (int g = 0; g < P.n_bgroup; ++g) {
+    const double idx = pref_val(P.bgroup[g], th);
+    double* fr = fac + ((long long)bl * P.n_bgroup + g) * P.n_toa;
+    for (int t = threadIdx.x; t < P.n_toa; t += 256) fr[t] = exp(idx * P.ln_chrom[t]);
+  }
   double acc = 0.0;
   for (int t = threadIdx.x; t < P.n_toa; t += 256) {
     const double ef = pref_val(P.slots[P.efac_slot[t]], th);
@@ -218,14 +228,20 @@ __global__ __launch_bounds__(256) void wn_weights_kernel(PsrDev P, const double*
 
 // s[bl][e][:] = sum_{t in epoch e} w_t T_aug[t][:]
 __global__ __launch_bounds__(256) void epoch_sums_kernel(PsrDev P, const double* __restrict__ w,
+                                                         const double* __restrict__ fac,
                                                          double* __restrict__ s) {
   const int e = blockIdx.x, bl = blockIdx.y;
   const double* wr = w + (long long)bl * P.n_toa;
   double* out = s + ((long long)bl * P.n_epoch + e) * P.ld;
   const int t0 = P.ep_start[e], t1 = P.ep_stop[e];
   for (int c = threadIdx.x; c < P.ld; c += 256) {
+    const int g = P.n_bgroup ? P.col_bgroup[c] : -1;
+    const double* fr = g >= 0 ? fac + ((long long)bl * P.n_bgroup + g) * P.n_toa : nullptr;
     double a = 0.0;
-    for (int t = t0; t < t1; ++t) a += wr[t] * P.T[(long long)t * P.ld + c];
+    for (int t = t0; t < t1; ++t) {
+      const double x = P.T[(long long)t * P.ld + c];
+      a += wr[t] * (g >= 0 ? x * fr[t] : x);
+    }
     out[c] = a;
   }
 }
@@ -242,6 +258,7 @@ template <int NB>
 __global__ __launch_bounds__(256) void contract_mfma_kernel(PsrDev P, const double* __restrict__ w,
                                                             const double* __restrict__ beta,
                                                             const double* __restrict__ s,
+                                                            const double* __restrict__ fac,
                                                             double* __restrict__ G) {
   constexpr int LD = 16 * NB;
   constexpr int NBLK = NB * (NB + 1) / 2;
@@ -275,8 +292,18 @@ __global__ __launch_bounds__(256) void contract_mfma_kernel(PsrDev P, const doub
     const double wsign = pass == 0 ? 1.0 : -1.0;
     for (int t0 = 0; t0 < nrows; t0 += CT_ROWS) {
       const int rows = min(CT_ROWS, nrows - t0);
-      for (int idx = threadIdx.x; idx < CT_ROWS * LD; idx += 256)
-        tile[idx] = idx < rows * LD ? src[(long long)t0 * LD + idx] : 0.0;
+      if (pass == 0 && P.n_bgroup) {   // theta-dependent chromatic columns: scale per TOA
+        for (int idx = threadIdx.x; idx < CT_ROWS * LD; idx += 256) {
+          const int r = idx / LD, cc = idx - r * LD;
+          double v = idx < rows * LD ? src[(long long)t0 * LD + idx] : 0.0;
+          const int g = P.col_bgroup[cc];
+          if (g >= 0 && r < rows) v *= fac[((long long)bl * P.n_bgroup + g) * P.n_toa + t0 + r];
+          tile[idx] = v;
+        }
+      } else {
+        for (int idx = threadIdx.x; idx < CT_ROWS * LD; idx += 256)
+          tile[idx] = idx < rows * LD ? src[(long long)t0 * LD + idx] : 0.0;
+      }
       if (threadIdx.x < CT_ROWS) wt[threadIdx.x] = threadIdx.x < rows ? wsign * wsrc[t0 + threadIdx.x] : 0.0;
       __syncthreads();
 #pragma unroll
@@ -666,7 +693,7 @@ struct ewh_handle {
   double* d_out = nullptr;
   size_t io_cap = 0;
   // varying-WN scratch
-  double *d_w = nullptr, *d_beta = nullptr, *d_s = nullptr, *d_G = nullptr, *d_Kb = nullptr;
+  double *d_w = nullptr, *d_beta = nullptr, *d_s = nullptr, *d_G = nullptr, *d_Kb = nullptr, *d_fac = nullptr;
   int chunk = 0;
   int last_B = 0;
 };
@@ -727,6 +754,13 @@ int validate(const ewh_pta_desc* d) {
       if (s.epoch_slot[e] < 0 || s.epoch_slot[e] >= s.n_slot) return set_err(EWH_E_INVALID, tag + "epoch slot out of range");
       prev = s.epoch_stop[e];
     }
+    if (s.n_bgroup < 0 || (s.n_bgroup > 0 && (!s.bgroup_idx || !s.col_bgroup || !s.ln_chrom)))
+      return set_err(EWH_E_INVALID, tag + "bad basis-group tables");
+    for (int g = 0; g < s.n_bgroup; ++g)
+      if (s.bgroup_idx[g].idx >= d->n_param) return set_err(EWH_E_INVALID, tag + "basis-group theta index out of range");
+    for (int j = 0; s.n_bgroup > 0 && j < s.n_col; ++j)
+      if (s.col_bgroup[j] < -1 || s.col_bgroup[j] >= s.n_bgroup || (j < s.n_lead_const && s.col_bgroup[j] >= 0))
+        return set_err(EWH_E_INVALID, tag + "bad column basis group");
     std::vector<int> cnt(s.n_col, 0);
     for (int e = 0; e < s.n_spec; ++e) {
       const ewh_spec_entry& sp = s.spec[e];
@@ -773,28 +807,29 @@ void build_csr(const ewh_pulsar_desc& s, int c0, int c1, std::vector<int>& ptr, 
 }
 
 template <int NB>
-void launch_contract(const PsrDev& P, const double* w, const double* beta, const double* s, double* G, int nb_samples,
-                     hipStream_t st) {
+void launch_contract(const PsrDev& P, const double* w, const double* beta, const double* s, const double* fac,
+                     double* G, int nb_samples, hipStream_t st) {
   const size_t lds = (size_t)(CT_ROWS * 16 * NB + CT_ROWS) * sizeof(double);
-  hipLaunchKernelGGL(HIP_KERNEL_NAME(contract_mfma_kernel<NB>), dim3(nb_samples), dim3(256), lds, st, P, w, beta, s, G);
+  hipLaunchKernelGGL(HIP_KERNEL_NAME(contract_mfma_kernel<NB>), dim3(nb_samples), dim3(256), lds, st, P, w, beta, s,
+                     fac, G);
 }
 
-int dispatch_contract(int nb, const PsrDev& P, const double* w, const double* beta, const double* s, double* G,
-                      int nb_samples, hipStream_t st) {
+int dispatch_contract(int nb, const PsrDev& P, const double* w, const double* beta, const double* s,
+                      const double* fac, double* G, int nb_samples, hipStream_t st) {
   switch (nb) {
-    case 1: launch_contract<1>(P, w, beta, s, G, nb_samples, st); break;
-    case 2: launch_contract<2>(P, w, beta, s, G, nb_samples, st); break;
-    case 3: launch_contract<3>(P, w, beta, s, G, nb_samples, st); break;
-    case 4: launch_contract<4>(P, w, beta, s, G, nb_samples, st); break;
-    case 5: launch_contract<5>(P, w, beta, s, G, nb_samples, st); break;
-    case 6: launch_contract<6>(P, w, beta, s, G, nb_samples, st); break;
-    case 7: launch_contract<7>(P, w, beta, s, G, nb_samples, st); break;
-    case 8: launch_contract<8>(P, w, beta, s, G, nb_samples, st); break;
-    case 9: launch_contract<9>(P, w, beta, s, G, nb_samples, st); break;
-    case 10: launch_contract<10>(P, w, beta, s, G, nb_samples, st); break;
-    case 11: launch_contract<11>(P, w, beta, s, G, nb_samples, st); break;
-    case 12: launch_contract<12>(P, w, beta, s, G, nb_samples, st); break;
-    case 13: launch_contract<13>(P, w, beta, s, G, nb_samples, st); break;
+    case 1: launch_contract<1>(P, w, beta, s, fac, G, nb_samples, st); break;
+    case 2: launch_contract<2>(P, w, beta, s, fac, G, nb_samples, st); break;
+    case 3: launch_contract<3>(P, w, beta, s, fac, G, nb_samples, st); break;
+    case 4: launch_contract<4>(P, w, beta, s, fac, G, nb_samples, st); break;
+    case 5: launch_contract<5>(P, w, beta, s, fac, G, nb_samples, st); break;
+    case 6: launch_contract<6>(P, w, beta, s, fac, G, nb_samples, st); break;
+    case 7: launch_contract<7>(P, w, beta, s, fac, G, nb_samples, st); break;
+    case 8: launch_contract<8>(P, w, beta, s, fac, G, nb_samples, st); break;
+    case 9: launch_contract<9>(P, w, beta, s, fac, G, nb_samples, st); break;
+    case 10: launch_contract<10>(P, w, beta, s, fac, G, nb_samples, st); break;
+    case 11: launch_contract<11>(P, w, beta, s, fac, G, nb_samples, st); break;
+    case 12: launch_contract<12>(P, w, beta, s, fac, G, nb_samples, st); break;
+    case 13: launch_contract<13>(P, w, beta, s, fac, G, nb_samples, st); break;
     default: return set_err(EWH_E_UNSUPPORTED, "basis too wide for the contraction kernel (> 207 columns)");
   }
   return 0;
@@ -863,20 +898,21 @@ int ensure_units(ewh_handle* h, int B) {
 int ensure_var_scratch(ewh_handle* h, int B) {
   if (h->white_fixed) return 0;
   if (h->chunk > 0 && (h->chunk >= B || h->chunk >= 1024)) return 0;
-  for (void* p : {(void*)h->d_w, (void*)h->d_beta, (void*)h->d_s, (void*)h->d_G, (void*)h->d_Kb}) {
+  for (void* p : {(void*)h->d_w, (void*)h->d_beta, (void*)h->d_s, (void*)h->d_G, (void*)h->d_Kb, (void*)h->d_fac}) {
     if (p) {
       hipFree(p);
       h->allocs.erase(std::find(h->allocs.begin(), h->allocs.end(), p));
     }
   }
-  size_t maxn = 1, maxe = 1, maxld = 16;
+  size_t maxn = 1, maxe = 1, maxld = 16, maxfac = 1;
   for (auto& ps : h->psr) {
     maxn = std::max(maxn, (size_t)ps.n_toa);
     maxe = std::max(maxe, (size_t)ps.n_epoch);
     maxld = std::max(maxld, (size_t)ps.ld);
+    maxfac = std::max(maxfac, (size_t)ps.n_toa * ps.dev.n_bgroup);
   }
   // chunk: keep G (ld^2) and s (E*ld) scratch under ~1.5 GB
-  const size_t per = (maxld * maxld + maxe * maxld + maxn + maxe + 1) * sizeof(double);
+  const size_t per = (maxld * maxld + maxe * maxld + maxn + maxe + maxfac + 1) * sizeof(double);
   size_t chunk = std::max<size_t>(1, (size_t)1536 * 1024 * 1024 / per);
   chunk = std::min<size_t>(chunk, std::min<size_t>(std::max(B, 1), 1024));
   int rc;
@@ -885,6 +921,7 @@ int ensure_var_scratch(ewh_handle* h, int B) {
   if ((rc = dalloc(h, &h->d_s, chunk * maxe * maxld))) return rc;
   if ((rc = dalloc(h, &h->d_G, chunk * maxld * maxld))) return rc;
   if ((rc = dalloc(h, &h->d_Kb, chunk))) return rc;
+  if ((rc = dalloc(h, &h->d_fac, chunk * maxfac))) return rc;
   h->chunk = (int)chunk;
   std::vector<CholJob> jobs(h->P);
   for (int p = 0; p < h->P; ++p) {
@@ -899,10 +936,11 @@ int ensure_var_scratch(ewh_handle* h, int B) {
 int run_white(ewh_handle* h, int p, const double* theta, int ldth, int b0, int nb) {
   PsrHost& ps = h->psr[p];
   hipLaunchKernelGGL(wn_weights_kernel, dim3(nb), dim3(256), 0, h->stream, ps.dev, theta, ldth, b0, h->d_w,
-                     h->d_beta, h->d_Kb);
+                     h->d_beta, h->d_Kb, h->d_fac);
   if (ps.n_epoch > 0)
-    hipLaunchKernelGGL(epoch_sums_kernel, dim3(ps.n_epoch, nb), dim3(256), 0, h->stream, ps.dev, h->d_w, h->d_s);
-  int rc = dispatch_contract(ps.nb, ps.dev, h->d_w, h->d_beta, h->d_s, h->d_G, nb, h->stream);
+    hipLaunchKernelGGL(epoch_sums_kernel, dim3(ps.n_epoch, nb), dim3(256), 0, h->stream, ps.dev, h->d_w, h->d_fac,
+                       h->d_s);
+  int rc = dispatch_contract(ps.nb, ps.dev, h->d_w, h->d_beta, h->d_s, h->d_fac, h->d_G, nb, h->stream);
   if (rc) return rc;
   EWH_HIP(hipGetLastError());
   return 0;
@@ -931,10 +969,11 @@ int setup_fixed(ewh_handle* h, const ewh_pta_desc* d) {
   std::vector<CholJob> jobs(h->P);
   for (int p = 0; p < h->P; ++p) {
     PsrHost& ps = h->psr[p];
-    hipLaunchKernelGGL(wn_weights_kernel, dim3(1), dim3(256), 0, h->stream, ps.dev, dummy_theta, 0, 0, w, beta, Kb);
+    hipLaunchKernelGGL(wn_weights_kernel, dim3(1), dim3(256), 0, h->stream, ps.dev, dummy_theta, 0, 0, w, beta, Kb,
+                       nullptr);
     if (ps.n_epoch > 0)
-      hipLaunchKernelGGL(epoch_sums_kernel, dim3(ps.n_epoch, 1), dim3(256), 0, h->stream, ps.dev, w, s);
-    if ((rc = dispatch_contract(ps.nb, ps.dev, w, beta, s, G, 1, h->stream))) return rc;
+      hipLaunchKernelGGL(epoch_sums_kernel, dim3(ps.n_epoch, 1), dim3(256), 0, h->stream, ps.dev, w, nullptr, s);
+    if ((rc = dispatch_contract(ps.nb, ps.dev, w, beta, s, nullptr, G, 1, h->stream))) return rc;
     double Kb_h = 0.0;
     EWH_HIP(hipMemcpyAsync(&Kb_h, Kb, sizeof(double), hipMemcpyDeviceToHost, h->stream));
     EWH_HIP(hipStreamSynchronize(h->stream));
@@ -990,7 +1029,7 @@ int ewh_create(const ewh_pta_desc* d, int device, ewh_handle** out) {
     ps.fx_nb = nb_for(ps.fx_m + 1);
     ps.fx_ld = 16 * ps.fx_nb;
     for (int i = 0; i < s.n_slot; ++i) ps.has_theta_white |= pref_uses_theta(s.slots[i]);
-    any_theta_white |= ps.has_theta_white;
+    any_theta_white |= ps.has_theta_white || s.n_bgroup > 0;
     // T_aug: [basis | 0-pad | r], row-major n x ld
     std::vector<double> Ta((size_t)s.n_toa * ps.ld, 0.0), sig2(s.n_toa);
     for (int t = 0; t < s.n_toa; ++t) {
@@ -1010,7 +1049,18 @@ int ewh_create(const ewh_pta_desc* d, int device, ewh_handle** out) {
     if ((rc = dupload(h, &d_es, s.epoch_start, (size_t)s.n_epoch))) return bail(rc);
     if ((rc = dupload(h, &d_ee, s.epoch_stop, (size_t)s.n_epoch))) return bail(rc);
     if ((rc = dupload(h, &d_eslot, s.epoch_slot, (size_t)s.n_epoch))) return bail(rc);
-    ps.dev = PsrDev{s.n_toa, s.n_col, ps.ld, ps.nb, s.n_epoch, dT, dsig2, d_ef, d_eq, d_slots, d_es, d_ee, d_eslot};
+    int* d_cbg = nullptr;
+    double* d_lnc = nullptr;
+    ewh_pref* d_bg = nullptr;
+    if (s.n_bgroup > 0) {
+      std::vector<int> cbg(ps.ld, -1);
+      for (int j = 0; j < s.n_col; ++j) cbg[j] = s.col_bgroup[j];
+      if ((rc = dupload(h, &d_cbg, cbg.data(), cbg.size()))) return bail(rc);
+      if ((rc = dupload(h, &d_lnc, s.ln_chrom, (size_t)s.n_toa))) return bail(rc);
+      if ((rc = dupload(h, &d_bg, s.bgroup_idx, (size_t)s.n_bgroup))) return bail(rc);
+    }
+    ps.dev = PsrDev{s.n_toa, s.n_col, ps.ld, ps.nb, s.n_epoch, dT, dsig2, d_ef, d_eq, d_slots, d_es, d_ee, d_eslot,
+                    s.n_bgroup, d_cbg, d_lnc, d_bg};
     std::vector<int> ptr;
     std::vector<DSpec> ent;
     build_csr(s, 0, s.n_col, ptr, ent);

@@ -167,6 +167,10 @@ class PTA:
         return all(isinstance(p, parameter.ConstantParameter)
                    for c in self._collections for w in c.white for p in w.params)
 
+    def basis_varies(self):
+        """True if some basis depends on theta (chromred 'vary'): no TNT cache."""
+        return any(c.basis_groups for c in self._collections)
+
     def layout(self):
         """Host-side per-pulsar tables for the engine (plain numpy)."""
         out = []
@@ -218,7 +222,10 @@ class PTA:
                         spec.append((_lib.SPEC_FREESPEC, j, ref, (-1, 0.0), (-1, 0.0), e["f"], 0.0))
                     else:
                         raise ValueError(e["kind"])
+            bgroups = [self._pref(p) for p in c.basis_groups]
             out.append(dict(name=c.name, T=np.ascontiguousarray(c.T, dtype=float),
+                            bgroups=bgroups, col_bgroup=np.ascontiguousarray(c.col_bgroup, np.int32),
+                            ln_chrom=np.ascontiguousarray(c.ln_chrom, dtype=float),
                             resid=np.ascontiguousarray(psr.residuals, dtype=float),
                             toaerr=np.ascontiguousarray(psr.toaerrs, dtype=float),
                             n_lead=c.n_lead_const, slots=slots, efac=efac, equad=equad,
@@ -268,16 +275,20 @@ class Engine:
             for k, (kind, col, p0, p1, p2, f, df) in enumerate(L["spec"]):
                 spec[k] = _lib.SpecEntry(kind, col, _lib.Pref(p0[0], 0, p0[1]), _lib.Pref(p1[0], 0, p1[1]),
                                          _lib.Pref(p2[0], 0, p2[1]), f, df, const.fyr)
+            bg = (_lib.Pref * max(1, len(L["bgroups"])))()
+            for k, (idx, cv) in enumerate(L["bgroups"]):
+                bg[k] = _lib.Pref(idx, 0, cv)
             arrs = [L["T"], L["resid"], L["toaerr"], L["efac"], L["equad"], L["ep_start"], L["ep_stop"],
-                    L["ep_slot"]]
-            keep.extend(arrs + [slots, spec])
+                    L["ep_slot"], L["col_bgroup"], L["ln_chrom"]]
+            keep.extend(arrs + [slots, spec, bg])
             descs[i] = _lib.PulsarDesc(
                 n, m, L["n_lead"], len(L["spec"]),
                 _as_ptr(L["T"], C.c_double), _as_ptr(L["resid"], C.c_double), _as_ptr(L["toaerr"], C.c_double),
                 len(L["slots"]), slots, _as_ptr(L["efac"], C.c_int32), _as_ptr(L["equad"], C.c_int32),
                 len(L["ep_start"]), _as_ptr(L["ep_start"], C.c_int32), _as_ptr(L["ep_stop"], C.c_int32),
-                _as_ptr(L["ep_slot"], C.c_int32), spec)
-        self.white_fixed = pta.white_fixed()
+                _as_ptr(L["ep_slot"], C.c_int32), spec,
+                len(L["bgroups"]), bg, _as_ptr(L["col_bgroup"], C.c_int32), _as_ptr(L["ln_chrom"], C.c_double))
+        self.white_fixed = pta.white_fixed() and not pta.basis_varies()
         d = _lib.PtaDesc(_lib.EWH_ABI_VERSION, len(lay), self.n_param, int(self.white_fixed), descs)
         h = C.c_void_p()
         _lib.check(self.lib.ewh_create(C.byref(d), int(device), C.byref(h)))

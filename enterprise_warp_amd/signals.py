@@ -91,11 +91,13 @@ def createfourierdesignmatrix_dm(nmodes=30, Tspan=None, fref=1400.0):
 
 
 def createfourierdesignmatrix_chromatic(nmodes=30, Tspan=None, idx=4.0):
-    """[ent] gp_bases.createfourierdesignmatrix_chromatic (enterprise_models.py:248-250)."""
-    if not isinstance(idx, (int, float, np.floating, np.integer)):
-        raise NotImplementedError("chromatic noise with a sampled index (chromred 'vary') makes the basis "
-                                  "theta-dependent; not in this round's device path (DESIGN.md §Scope)")
-    return BasisSpec("chromatic", nmodes, Tspan, idx=float(idx))
+    """[ent] gp_bases.createfourierdesignmatrix_chromatic (enterprise_models.py:248-250):
+    F * (1400 / nu)^idx.  A sampled idx (chromred 'vary') makes the basis
+    theta-dependent: its columns are never merged and are rescaled per
+    sample on the device (contraction kernels)."""
+    if isinstance(idx, (int, float, np.floating, np.integer)):
+        idx = float(idx)
+    return BasisSpec("chromatic", nmodes, Tspan, idx=idx)
 
 
 def fourier_matrix(toas, nmodes, Tspan):
@@ -108,11 +110,13 @@ def fourier_matrix(toas, nmodes, Tspan):
 
 
 def build_basis(spec, toas, freqs):
+    """Basis of one GP on the selected TOAs; a sampled chromatic index leaves
+    the Fourier columns unscaled (scaled per sample on the device)."""
     Ts = spec.Tspan if spec.Tspan is not None else toas.max() - toas.min()
     F, Ff = fourier_matrix(toas, spec.nmodes, Ts)
     if spec.kind == "dm":
         F = F * ((float(spec.fref) / freqs) ** 2)[:, None]
-    elif spec.kind == "chromatic":
+    elif spec.kind == "chromatic" and isinstance(spec.idx, float):
         F = F * ((1400.0 / freqs) ** spec.idx)[:, None]
     return F, Ff, Ts
 
@@ -272,7 +276,12 @@ class _BoundGP:
                 if sig.spectrum.kind == "free_spectrum" and (p.size or 1) != Fm.shape[1] // 2:
                     raise ValueError(f"{p.name}: size {p.size} != number of frequencies {Fm.shape[1] // 2}")
                 pars[loc] = p
-            self.parts.append({"key": key, "F": F, "f": Ff, "Tspan": Ts, "pars": pars, "explicit": explicit})
+            bpar = None
+            if sig.basis.kind == "chromatic" and not isinstance(sig.basis.idx, float):
+                bpar = parameter.resolve(sig.basis.idx, _pname(psr.name, sig.name, key, "idx"))
+                self.params.append(bpar)
+            self.parts.append({"key": key, "F": F, "f": Ff, "Tspan": Ts, "pars": pars, "explicit": explicit,
+                               "basis_par": bpar})
             self.params.extend(pars.values())
 
     def spec(self):
@@ -280,7 +289,7 @@ class _BoundGP:
         b = self.basis_spec
         for part in self.parts:
             d = {"kind": "gp", "name": self.name, "basis": b.kind, "nfreqs": b.nmodes, "Tspan": part["Tspan"],
-                 "fref": float(b.fref), "idx": float(b.idx), "spectrum": self.spectrum.kind,
+                 "fref": float(b.fref), "idx": float(b.idx) if part["basis_par"] is None else None, "spectrum": self.spectrum.kind,
                  "components": self.spectrum.components, "pnames": {}, "const": {},
                  "selection": None if self.sel_flag is None else {"flag": self.sel_flag, "value": self.sel_value}}
             for loc, p in part["pars"].items():
@@ -288,6 +297,8 @@ class _BoundGP:
                     d["const"][loc] = p.value
                 elif part["explicit"][loc]:
                     d["pnames"][loc] = p.name
+            if part["basis_par"] is not None:
+                d["idx_param"] = part["basis_par"].name
             out.append(d)
         return out
 
@@ -334,6 +345,7 @@ class SignalCollection:
         cols = []          # merged basis columns
         entries = []       # per column: list of entry dicts
         by_hash = {}       # column bytes -> candidate indices (same result as a linear np.array_equal scan)
+        self.col_bgroup_map = {}   # column -> chromatic-index Parameter (theta-dependent basis)
         self.n_tm = 0
         seen_gp = False
 
@@ -361,10 +373,24 @@ class SignalCollection:
                     f = part["f"]
                     df = np.repeat(np.diff(np.concatenate((np.array([0]), f[::comp]))), comp)
                     for j in range(part["F"].shape[1]):
-                        add(part["F"][:, j], {"kind": b.spectrum.kind, "pars": part["pars"], "f": f[j],
-                                              "df": df[j], "mode": j // 2})
+                        e = {"kind": b.spectrum.kind, "pars": part["pars"], "f": f[j], "df": df[j], "mode": j // 2}
+                        if part["basis_par"] is None:
+                            add(part["F"][:, j], e)
+                        else:   # theta-dependent basis: own column, never merged
+                            cols.append(part["F"][:, j])
+                            entries.append([e])
+                            self.col_bgroup_map[len(cols) - 1] = part["basis_par"]
         self.T = np.array(cols).T if cols else np.zeros((n, 0))
         self.entries = entries
+        # theta-dependent basis groups: one per chromatic-index parameter
+        self.basis_groups = []
+        self.col_bgroup = np.full(len(cols), -1, np.int32)
+        for j, p in sorted(self.col_bgroup_map.items()):
+            names = [q.name for q in self.basis_groups]
+            if p.name not in names:
+                self.basis_groups.append(p)
+            self.col_bgroup[j] = [q.name for q in self.basis_groups].index(p.name)
+        self.ln_chrom = np.log(1400.0 / np.asarray(psr.freqs, float))
         # leading columns whose phi is constant (timing model): eliminated once when white noise is fixed
         nl = 0
         while nl < len(entries) and all(e["kind"] == "const" for e in entries[nl]):

@@ -49,7 +49,7 @@
 extern "C" {
 #endif
 
-#define EWH_ABI_VERSION 1
+#define EWH_ABI_VERSION 2
 
 enum ewh_status {
   EWH_OK = 0,
@@ -108,6 +108,15 @@ typedef struct ewh_pulsar_desc {
   const int32_t* epoch_stop;  /* n_epoch, one past the last TOA */
   const int32_t* epoch_slot;  /* n_epoch: slot of log10_ecorr */
   const ewh_spec_entry* spec; /* n_spec */
+  /* theta-dependent basis columns ([ent] BasisGP with basis parameters:
+   * chromred 'vary', enterprise_models.py:242-252): column j of group g =
+   * col_bgroup[j] >= 0 is used as basis[t][j] * exp(idx_g * ln_chrom[t]),
+   * idx_g = bgroup_idx[g], i.e. F * (1400 / nu)^idx.  A pulsar with groups
+   * is always evaluated on the varying path (no T^T N^-1 T cache). */
+  int32_t n_bgroup;
+  const ewh_pref* bgroup_idx;   /* n_bgroup */
+  const int32_t* col_bgroup;    /* n_col (-1: fixed column); NULL if n_bgroup == 0 */
+  const double* ln_chrom;       /* n_toa: ln(1400 MHz / nu_t); NULL if n_bgroup == 0 */
 } ewh_pulsar_desc;
 
 typedef struct ewh_pta_desc {

@@ -31,7 +31,8 @@ def dense_lnl(oracle_pulsar, params, tm_var=None):
         for g in pp.gps:
             if g["kind"] == "tm":
                 phi[g["idx"]] = tm_var
-    C += (pp.T * phi[None, :]) @ pp.T.T
+    T = pp.basis(params)
+    C += (T * phi[None, :]) @ T.T
     cf = sl.cho_factor(C, lower=True)
     x = sl.cho_solve(cf, pp.r)
     return -0.5 * np.dot(pp.r, x) - np.sum(np.log(np.diag(cf[0])))

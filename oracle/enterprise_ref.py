@@ -16,6 +16,7 @@ enterprise_warp.init_pta assembles them at enterprise_warp.py:453-500):
   {"kind": "gp", "name": str, "basis": "fourier"|"dm"|"chromatic",
    "nfreqs": int, "Tspan": float, "fref": float, "idx": float,
    "spectrum": "powerlaw"|"turnover"|"free_spectrum", "components": 2,
+   "idx_param": name (chromatic basis with a sampled index),
    "pnames": {local: global name} (explicitly named parameters, e.g. gw_*),
    "const": {local: value}, "selection": None | {"flag": f, "value": v}}
 
@@ -150,6 +151,7 @@ class OraclePulsar:
         n = len(self.r)
         self.white = []        # (kind, {key: mask}, {key: pname})
         self.gps = []          # dict per GP signal
+        self.basis_params = []  # (columns, unscaled F, idx parameter name) of theta-dependent bases
         self.has_tm = False
         cols = []              # unique basis columns (SignalCollection._combine_basis_columns)
         for t in terms:
@@ -213,13 +215,22 @@ class OraclePulsar:
                 Fm, Ff = fourier_basis(tt, nf, Ts)
             elif t["basis"] == "dm":
                 Fm, Ff = dm_basis(tt, np.asarray(psr.freqs)[mask], nf, Ts, float(t.get("fref", 1400.0)))
+            elif t["basis"] == "chromatic" and "idx_param" in t:
+                # basis depends on theta ([ent] BasisGP with basis_params):
+                # columns are appended unmerged and rebuilt on every call
+                Fm, Ff = fourier_basis(tt, nf, Ts)
             elif t["basis"] == "chromatic":
                 Fm, Ff = chromatic_basis(tt, np.asarray(psr.freqs)[mask], nf, Ts, float(t.get("idx", 4.0)))
             else:
                 raise ValueError(t["basis"])
             F = np.zeros((n, Fm.shape[1]))
             F[mask] = Fm
-            idx = [self._add_cols(cols, F[:, j]) for j in range(F.shape[1])]
+            if "idx_param" in t:
+                idx = list(range(len(cols), len(cols) + F.shape[1]))
+                cols.extend(F[:, j] for j in range(F.shape[1]))
+                self.basis_params.append((idx, F, t["idx_param"]))
+            else:
+                idx = [self._add_cols(cols, F[:, j]) for j in range(F.shape[1])]
             names = {}
             for p in {"powerlaw": ["log10_A", "gamma"], "turnover": ["log10_A", "gamma", "fc"],
                       "free_spectrum": ["log10_rho"]}[t["spectrum"]]:
@@ -318,11 +329,23 @@ class OraclePulsar:
                 Nx[slc] -= beta * np.dot(ni, x[slc]) * ni
         return np.dot(T.T, Nx)
 
+    def basis(self, params):
+        """[ent] SignalCollection.get_basis: theta-dependent chromatic columns
+        F * (1400 / nu)^idx rebuilt from the current idx."""
+        if not self.basis_params:
+            return self.T
+        T = self.T.copy()
+        nu = np.asarray(self.psr.freqs, float)
+        for idx, F, pn in self.basis_params:
+            T[:, idx] = F * ((1400.0 / nu) ** params[pn])[:, None]
+        return T
+
     def white_terms(self, params):
         """[ent] get_TNT / get_TNr / get_rNr_logdet."""
         D, ep = self._sm(params)
-        TNT = self._solve_2D2(D, ep, self.T, self.T)
-        TNr = self._solve_2D1(D, ep, self.T, self.r)
+        T = self.basis(params)
+        TNT = self._solve_2D2(D, ep, T, T)
+        TNr = self._solve_2D1(D, ep, T, self.r)
         rNr, ldN = self._solve_1D1(D, ep, self.r)
         return TNT, TNr, rNr, ldN
 
@@ -337,7 +360,7 @@ class OraclePTA:
     def __init__(self, psrs, terms_per_psr, fixed_params=None):
         self.pulsars = [OraclePulsar(p, t) for p, t in zip(psrs, terms_per_psr)]
         self.fixed = None
-        if fixed_params is not None:
+        if fixed_params is not None and not any(pp.basis_params for pp in self.pulsars):
             self.fixed = [pp.white_terms(fixed_params) for pp in self.pulsars]
 
     def lnlikelihood(self, params):

@@ -50,7 +50,7 @@ def load_golden(name):
     return pta, z["theta"], z["lnl"], z["min_eig"]
 
 
-GOLDEN_NAMES = ["c1_j1832", "c1_turnover", "c2_small", "c3_small", "c3_freesp", "c4_small"]
+GOLDEN_NAMES = ["c1_j1832", "c1_turnover", "c2_small", "c2_chromvary", "c3_small", "c3_freesp", "c4_small"]
 
 
 def gpu_available():

@@ -127,6 +127,18 @@ def main():
                                             "spin_noise": "powerlaw_30_nfreqs", "dm_noise": "powerlaw_30_nfreqs",
                                             "ppta_band_noise": ["20CM_30_nfreqs"]},
                                        {"gwb": "vary_gamma_14_nfreqs"}, False), X)
+    # c2 chromatic: varying white noise, DM noise and a chromatic GP whose
+    # spectral index is sampled (chromred "vary": the basis depends on theta)
+    c2c = synth.config_c2(n_toa=1200, epoch_size=4)
+    psr = c2c.pta.signal_collections[0].psr
+    ns = synth.params_namespace(np.ptp(psr.toas), False)
+    terms_c = {"efac": "by_backend", "equad": "by_backend", "ecorr": "by_backend",
+               "spin_noise": "powerlaw_20_nfreqs", "dm_noise": "powerlaw_20_nfreqs", "chromred": "vary_15_nfreqs"}
+    pta_c = synth.build_pta([psr], terms_c, {}, ns, None)
+    truth_c = synth.truth_values(pta_c, 7)
+    X = np.vstack([synth.prior_draws(pta_c, 8, 17), synth.near_draws(pta_c, truth_c, 8, 18)])
+    dump("c2_chromvary", pta_c, {"per_psr_terms": terms_c, "common_terms": {}, "Tspan": float(np.ptp(psr.toas)),
+                                 "fixed_white": False, "noisedict": {}}, X)
 
 
 if __name__ == "__main__":

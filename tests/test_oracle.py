@@ -81,6 +81,42 @@ def test_woodbury_matches_dense(tm_var):
     assert abs(a - b) <= 1e-10 * abs(a)
 
 
+def test_woodbury_matches_dense_chromatic_vary():
+    """theta-dependent chromatic basis: the Woodbury route with the rebuilt
+    basis == the dense covariance built from the same basis."""
+    pta, X, _, _ = load_golden("c2_chromvary")
+    o = oracle_for(pta)
+    pp = o.pulsars[0]
+    assert pp.basis_params
+    const_ = pta.constant_values()
+    for x in X[8:11]:
+        d = dict(const_)
+        d.update(pta.map_params(x))
+        a = dense_lnl(pp, d, tm_var=1e-12)
+        b = woodbury_lnl(pp, d, tm_var=1e-12)
+        assert abs(a - b) <= 1e-9 * abs(a)
+
+
+def test_chromatic_vary_equals_fixed_index():
+    """A sampled chromatic index evaluated at idx = 4 reproduces the fixed
+    idx = 4 model (enterprise_models.py chromred option "vary" vs "4")."""
+    pta, X, _, _ = load_golden("c2_chromvary")
+    psr = pta.signal_collections[0].psr
+    ns = synth.params_namespace(np.ptp(psr.toas), False)
+    terms = {"efac": "by_backend", "equad": "by_backend", "ecorr": "by_backend",
+             "spin_noise": "powerlaw_20_nfreqs", "dm_noise": "powerlaw_20_nfreqs", "chromred": "4_15_nfreqs"}
+    pta4 = synth.build_pta([psr], terms, {}, ns, None)
+    ov, o4 = oracle_for(pta), oracle_for(pta4)
+    idx_name = [n for n in pta.param_names if n.endswith("_idx")]
+    assert len(idx_name) == 1 and len(pta4.param_names) == len(pta.param_names) - 1
+    for x in X[8:12]:
+        d = pta.map_params(x)
+        d[idx_name[0]] = 4.0
+        d4 = {k: v for k, v in d.items() if k != idx_name[0]}
+        la, lb = ov.lnlikelihood(d), o4.lnlikelihood(d4)
+        assert abs(la - lb) <= 1e-8 * abs(la)
+
+
 @pytest.mark.parametrize("name", GOLDEN_NAMES)
 def test_oracle_reproduces_golden(name):
     pta, X, lnl, _ = load_golden(name)
