@@ -135,6 +135,15 @@ __device__ __forceinline__ double rsqrt_nr(double a) {
   return fma(y, t, y);
 }
 
+// 1/a: hardware estimate + two Newton steps (~1 ulp).
+__device__ __forceinline__ double rcp_nr(double a) {
+  double y = __builtin_amdgcn_rcp(a);
+  double e = fma(-a, y, 1.0);
+  y = fma(y, e, y);
+  e = fma(-a, y, 1.0);
+  return fma(y, e, y);
+}
+
 __device__ __forceinline__ double wave_sum(double v) {
 #pragma unroll
   for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o);
@@ -499,7 +508,14 @@ __device__ __forceinline__ void syrk_update(v4d& C, const v4d& Ui, const v4d& Uj
 // W: waves per SIMD the register budget is cut for (2 -> 256 VGPRs: the NB = 8
 // three-phase kernel fits with no spills, so two units share each SIMD and one's
 // MFMAs overlap the other's VALU / LDS latency).
-template <int NB, int FULL, int W>
+// ALG: panel form.  0 = Cholesky panel (row k scaled by 1/sqrt(pivot) before it
+// is broadcast); 1 = square-root-free LDL^T panel: row k is broadcast raw while
+// 1/d_k is formed, the lane's rows take the update with u_i = A_ki / d_k, and
+// the 16 rows of the block row are scaled to U = D^-1/2 V together at the end
+// (one vector rsqrt per register instead of one serial rsqrt per pivot).  The
+// per-pivot dependency chain drops the scale -> ds_bpermute leg; log|Sigma| =
+// sum log d_k is accumulated per block row from the lanes' own pivots.
+template <int NB, int FULL, int W, int ALG = 0>
 __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(W, W)))
 void chol_mfma_kernel(const CholJob* __restrict__ jobs, int B, long long u0, int b_off,
                       const double* __restrict__ theta, int ldth, double* __restrict__ out_units) {
@@ -507,6 +523,7 @@ void chol_mfma_kernel(const CholJob* __restrict__ jobs, int B, long long u0, int
   using S = Split<NB>;
   constexpr int H = S::H;
   __shared__ double phinv[LD];
+  __shared__ double rowbuf[ALG == 2 ? 2 * LD : 1];   // ALG 2: double-buffered row-k broadcast
   const int lane = threadIdx.x;
   const int q = lane >> 4, c = lane & 15;
   const long long u = u0 + blockIdx.x;
@@ -546,8 +563,98 @@ void chol_mfma_kernel(const CholJob* __restrict__ jobs, int B, long long u0, int
 
   LogAcc ldet;
   bool ok = true;
+  // LDL^T panel row bb (ALG >= 1)
+  auto panel_ldl = [&](auto BBc, auto&& blk) {
+    constexpr int bb = decltype(BBc)::value;
+    static_for<0, 4>([&](auto KR) {
+      constexpr int kr = decltype(KR)::value;
+      auto step = [&](const int kq) {
+        const int k = 4 * kr + kq;
+        const double d = readlane_d(blk(BBc)[kr], 16 * kq + k);            // wave-uniform pivot
+        // raw row k: A[k][q + 4r] for this lane's rows (masked to rows > k) and
+        // A[k][col c] of every block of the row; both in flight while 1/d forms
+        double ui[4];
+        double rk[NB];
+        if constexpr (ALG == 2) {
+          // LDS broadcast: the 16 lanes of quad kq store row k of every block
+          // (one ds_write_b64 per block), every lane reads it back with 16
+          // distinct addresses per read (broadcast, bank-conflict free) --
+          // several times cheaper on the CU's LDS than two ds_bpermute_b32
+          // per double.  One wave per workgroup and LDS ops of a wave run in
+          // order, so no barrier: the asm fences only stop the compiler from
+          // moving the reads above the other lanes' writes.
+          double* rb = rowbuf + (k & 1) * LD;
+          if (q == kq) {
+            static_for<bb, NB>([&](auto JJ) {
+              constexpr int j = decltype(JJ)::value;
+              rb[16 * j + c] = blk(JJ)[kr];
+            });
+          }
+          asm volatile("" ::: "memory");
+          static_for<kr, 4>([&](auto R) {
+            constexpr int r = decltype(R)::value;
+            const double v = rb[16 * bb + q + 4 * r];
+            ui[r] = (r > kr || q > kq) ? v : 0.0;
+          });
+          static_for<bb, NB>([&](auto JJ) {
+            constexpr int j = decltype(JJ)::value;
+            rk[j] = rb[16 * j + c];
+          });
+          asm volatile("" ::: "memory");
+        } else {
+          static_for<kr, 4>([&](auto R) {
+            constexpr int r = decltype(R)::value;
+            const double v = __shfl(blk(BBc)[kr], 16 * kq + q + 4 * r);
+            ui[r] = (r > kr || q > kq) ? v : 0.0;
+          });
+          static_for<bb, NB>([&](auto JJ) {
+            constexpr int j = decltype(JJ)::value;
+            rk[j] = __shfl(blk(JJ)[kr], 16 * kq + c);
+          });
+        }
+        const double dinv = rcp_nr(d);
+        static_for<kr, 4>([&](auto R) { ui[decltype(R)::value] *= dinv; });
+        static_for<bb, NB>([&](auto JJ) {
+          constexpr int j = decltype(JJ)::value;
+          static_for<kr, 4>([&](auto R) {
+            constexpr int r = decltype(R)::value;
+            blk(JJ)[r] = fma(-ui[r], rk[j], blk(JJ)[r]);
+          });
+        });
+      };
+      constexpr int nk = (bb == NB - 1 && kr == 3) ? 3 : 4;   // the r column is not pivoted
+      if constexpr (FULL) {
+        static_for<0, nk>([&](auto KQ) {
+          step(decltype(KQ)::value);
+          // unrolled LDS-broadcast steps: keep the scheduler from hoisting the
+          // next steps' LDS reads (it otherwise spills ~1 KB per lane)
+          if constexpr (ALG == 2) __builtin_amdgcn_sched_barrier(0);
+        });
+      } else {
+#pragma unroll 1
+        for (int kq = 0; kq < nk; ++kq) step(kq);
+      }
+    });
+    // rows of the block row -> U = d^-1/2 V, d of row q + 4r read from the
+    // diagonal (lane 17q + 4r); log-det and positivity from one lane per row
+    // (c == 0); the r row (last block, row 15) is left as it is
+    static_for<0, 4>([&](auto R) {
+      constexpr int r = decltype(R)::value;
+      const bool rrow = (bb == NB - 1 && r == 3) && q == 3;
+      const double dg = __shfl(blk(BBc)[r], 17 * q + 4 * r);
+      const double dv = rrow ? 1.0 : dg;
+      ok = ok && (dv > 0.0);
+      if (c == 0) ldet.add(dv);
+      const double rs = rrow ? 1.0 : rsqrt_nr(dv);
+      static_for<bb, NB>([&](auto JJ) { blk(JJ)[r] *= rs; });
+    });
+  };
   // panel row bb over the blocks blk(j), j = bb..NB-1
   auto panel = [&](auto BBc, auto&& blk) {
+    if constexpr (ALG >= 1) {
+      panel_ldl(BBc, blk);
+      return;
+    }
     constexpr int bb = decltype(BBc)::value;
     static_for<0, 4>([&](auto KR) {
       constexpr int kr = decltype(KR)::value;
@@ -638,9 +745,15 @@ void chol_mfma_kernel(const CholJob* __restrict__ jobs, int B, long long u0, int
     });
   });
   const double qv = readlane_d(U2[S::i2(NB - 1, NB - 1)][3], 63);
+  double ldet_v = ldet.value();
+  bool ok_all = ok;
+  if constexpr (ALG >= 1) {          // per-lane partial log-dets and checks
+    ldet_v = wave_sum(ldet_v);
+    ok_all = __all(ok);
+  }
   if (lane == 0) {
-    double lnl = J.K[(long long)(b - b_off) * J.kstride] - 0.5 * qv - 0.5 * ldet.value() - 0.5 * lphi_sum;
-    if (!ok || J.fail) lnl = -INFINITY;
+    double lnl = J.K[(long long)(b - b_off) * J.kstride] - 0.5 * qv - 0.5 * ldet_v - 0.5 * lphi_sum;
+    if (!ok_all || J.fail) lnl = -INFINITY;
     out_units[(long long)p * B + b] = lnl;
   }
 }
@@ -837,37 +950,48 @@ int dispatch_contract(int nb, const PsrDev& P, const double* w, const double* be
 
 constexpr int default_waves(int nb) { return nb <= 8 ? 2 : 1; }
 
-template <int NB, int FULL = 0, int W = default_waves(NB)>
+template <int NB, int FULL = 0, int W = default_waves(NB), int ALG = 0>
 void launch_chol_mfma(const CholJob* jobs, int B, long long u0, long long n, int b_off, const double* theta, int ldth,
                       double* units, hipStream_t st) {
-  hipLaunchKernelGGL(HIP_KERNEL_NAME(chol_mfma_kernel<NB, FULL, W>), dim3((unsigned)n), dim3(64), 0, st, jobs, B, u0,
-                     b_off, theta, ldth, units);
+  hipLaunchKernelGGL(HIP_KERNEL_NAME(chol_mfma_kernel<NB, FULL, W, ALG>), dim3((unsigned)n), dim3(64), 0, st, jobs, B,
+                     u0, b_off, theta, ldth, units);
 }
 
 int dispatch_chol(int mode, int nb, int mreal, const CholJob* jobs, int B, long long u0, long long n, int b_off,
                   const double* theta, int ldth, double* units, hipStream_t st) {
   if (n <= 0) return 0;
-  if (mode == 2 && nb == 8) {   // A/B: fully unrolled panel steps
-    launch_chol_mfma<8, 1>(jobs, B, u0, n, b_off, theta, ldth, units, st);
-    return 0;
-  }
-  if (mode == 3 && nb == 8) {   // A/B: one wave per SIMD (512-register budget)
-    launch_chol_mfma<8, 0, 1>(jobs, B, u0, n, b_off, theta, ldth, units, st);
-    return 0;
-  }
-  if (mode != 1 && nb <= MFMA_NB_MAX) {
-    switch (nb) {
-      case 1: launch_chol_mfma<1>(jobs, B, u0, n, b_off, theta, ldth, units, st); return 0;
-      case 2: launch_chol_mfma<2>(jobs, B, u0, n, b_off, theta, ldth, units, st); return 0;
-      case 3: launch_chol_mfma<3>(jobs, B, u0, n, b_off, theta, ldth, units, st); return 0;
-      case 4: launch_chol_mfma<4>(jobs, B, u0, n, b_off, theta, ldth, units, st); return 0;
-      case 5: launch_chol_mfma<5>(jobs, B, u0, n, b_off, theta, ldth, units, st); return 0;
-      case 6: launch_chol_mfma<6>(jobs, B, u0, n, b_off, theta, ldth, units, st); return 0;
-      case 7: launch_chol_mfma<7>(jobs, B, u0, n, b_off, theta, ldth, units, st); return 0;
-      case 8: launch_chol_mfma<8>(jobs, B, u0, n, b_off, theta, ldth, units, st); return 0;
-      case 9: launch_chol_mfma<9>(jobs, B, u0, n, b_off, theta, ldth, units, st); return 0;
+  // A/B variants (NB = 8, the C3 reduced width); see ewh_set_kernel_mode
+  if (nb == 8 && mode >= 3) {
+    switch (mode) {
+      case 3: launch_chol_mfma<8, 1, 1, 1>(jobs, B, u0, n, b_off, theta, ldth, units, st); return 0;  // 1 wave/SIMD
+      case 4: launch_chol_mfma<8, 0, 2, 1>(jobs, B, u0, n, b_off, theta, ldth, units, st); return 0;  // LDL, looped
+      case 5: launch_chol_mfma<8, 1, 2, 0>(jobs, B, u0, n, b_off, theta, ldth, units, st); return 0;  // Cholesky, unrolled
+      case 6: launch_chol_mfma<8, 0, 2, 2>(jobs, B, u0, n, b_off, theta, ldth, units, st); return 0;  // LDL, LDS bcast
       default: break;
     }
+  }
+  if (mode != 1 && nb <= MFMA_NB_MAX) {
+    // default: LDL^T panel, panel steps unrolled up to NB = 8; mode 2: the
+    // round-1 Cholesky panel (looped) as the A/B baseline
+    const bool base = mode == 2;
+#define EWH_CHOL_CASE(NBV)                                                                            \
+  case NBV:                                                                                          \
+    if (base) launch_chol_mfma<NBV, 0, default_waves(NBV), 0>(jobs, B, u0, n, b_off, theta, ldth, units, st); \
+    else launch_chol_mfma<NBV, (NBV <= 8), default_waves(NBV), 1>(jobs, B, u0, n, b_off, theta, ldth, units, st); \
+    return 0;
+    switch (nb) {
+      EWH_CHOL_CASE(1)
+      EWH_CHOL_CASE(2)
+      EWH_CHOL_CASE(3)
+      EWH_CHOL_CASE(4)
+      EWH_CHOL_CASE(5)
+      EWH_CHOL_CASE(6)
+      EWH_CHOL_CASE(7)
+      EWH_CHOL_CASE(8)
+      EWH_CHOL_CASE(9)
+      default: break;
+    }
+#undef EWH_CHOL_CASE
   }
   const size_t lds = lds_bytes_chol(mreal);
   if (lds > LDS_MAX - 64) return set_err(EWH_E_UNSUPPORTED, "reduced matrix too large for the LDS Cholesky kernel");
@@ -1081,7 +1205,7 @@ int ewh_create(const ewh_pta_desc* d, int device, ewh_handle** out) {
 }
 
 int ewh_set_kernel_mode(ewh_handle* h, int32_t mode) {
-  if (!h || mode < 0 || mode > 3) return set_err(EWH_E_INVALID, "bad handle / mode");
+  if (!h || mode < 0 || mode > 6) return set_err(EWH_E_INVALID, "bad handle / mode");
   h->kernel_mode = mode;
   return 0;
 }

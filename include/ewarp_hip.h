@@ -151,10 +151,12 @@ int ewh_last_unit_terms(ewh_handle* h, double* out_host, int32_t B);
 /* Cost model used for sharding: relative cost of one unit of pulsar p. */
 double ewh_unit_cost(const ewh_handle* h, int32_t pulsar);
 
-/* Kernel selection: 0 = auto (MFMA register-blocked Cholesky when the
- * reduced matrix fits, LDS kernel otherwise), 1 = force the LDS kernel,
- * 2 = MFMA kernel with fully unrolled panel steps, 3 = MFMA kernel at one
- * wave per SIMD (A/B experiments; NB = 8 only, else as 0). */
+/* Kernel selection: 0 = auto (register-blocked MFMA factorisation with the
+ * LDL^T panel when the reduced matrix fits, LDS kernel otherwise), 1 = force
+ * the LDS kernel, 2 = the round-1 MFMA kernel (Cholesky panel, looped steps).
+ * A/B variants for NB = 8 only (else as 0): 3 = LDL^T at one wave per SIMD,
+ * 4 = LDL^T with looped steps, 5 = Cholesky panel with unrolled steps,
+ * 6 = LDL^T with the row broadcast through LDS. */
 int ewh_set_kernel_mode(ewh_handle* h, int32_t mode);
 
 void ewh_destroy(ewh_handle* h);

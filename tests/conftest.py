@@ -33,6 +33,29 @@ def lnl_tolerance(ref, min_eig=None):
     return tol
 
 
+def oracle_lnl_cond(pta, X):
+    """Oracle lnL per sample and the sample's conditioning (min over pulsars
+    of the smallest eigenvalue of the unit-diagonal-scaled Sigma), as the
+    golden fixtures store it (tests/golden/make_golden.py)."""
+    from oracle.enterprise_ref import OraclePTA
+    const = pta.constant_values()
+    fixed = const if pta.white_fixed() else None
+    o = OraclePTA([c.psr for c in pta.signal_collections], pta.oracle_terms(), fixed_params=fixed)
+    out, cond = [], []
+    for x in X:
+        d = dict(const)
+        d.update(pta.map_params(x))
+        out.append(o.lnlikelihood(d))
+        mins = []
+        for i, pp in enumerate(o.pulsars):
+            TNT = o.fixed[i][0] if o.fixed is not None else pp.white_terms(d)[0]
+            S = TNT + np.diag(1.0 / pp.phi(d))
+            sc = 1.0 / np.sqrt(np.diag(S))
+            mins.append(np.linalg.eigvalsh(S * sc[:, None] * sc[None, :])[0])
+        cond.append(min(mins))
+    return np.array(out), np.array(cond)
+
+
 def load_golden(name):
     """Rebuild (pta, theta, lnl, min_eig) from a committed fixture."""
     from enterprise_warp_amd import synth

@@ -61,3 +61,27 @@ def test_c3_pulsar_permutation_invariance(require_gpu, c3):
     rev = PTA(list(reversed(pta.signal_collections)))
     b = rev.get_lnlikelihood_batch(X)
     assert np.all(np.abs(a - b) <= lnl_tolerance(a))
+
+
+@pytest.mark.parametrize("mode", [0, 2, 3, 4, 5, 6])
+def test_c3_chol_variants_vs_oracle(require_gpu, c3, mode):
+    """Every register-blocked Cholesky variant (Cholesky / LDL^T panel, looped
+    / unrolled, 1-2 waves per SIMD) against the oracle on full-size C3: near-
+    truth draws at the strict bound, prior draws (loud red noise, Sigma close
+    to singular) at the conditioning-widened bound of conftest.lnl_tolerance."""
+    from conftest import oracle_lnl_cond
+    pta = c3.pta
+    X = np.concatenate([synth.near_draws(pta, c3.truth, 16, 7), synth.prior_draws(pta, 16, 8)])
+    pta.engine().set_kernel_mode(mode)
+    try:
+        got = pta.get_lnlikelihood_batch(X)
+    finally:
+        pta.engine().set_kernel_mode(0)
+    want, cond = oracle_lnl_cond(pta, X)
+    fin = np.isfinite(want)
+    strict = np.arange(len(X)) < 16
+    err = np.abs(got - want)
+    assert np.all(err[strict] <= lnl_tolerance(want[strict])), f"mode {mode}: near-truth worst {err[strict].max():.3e}"
+    tol = lnl_tolerance(want[fin], cond[fin])
+    assert np.all(err[fin] <= tol), f"mode {mode}: worst err/tol {np.max(err[fin] / tol):.3e}"
+    assert np.array_equal(np.isfinite(got), fin)
