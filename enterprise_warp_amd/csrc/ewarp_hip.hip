@@ -165,6 +165,8 @@ __device__ double block_sum256(double v, double* scratch) {
 // ----------------------------------------------------------------------------
 // per-pulsar device tables
 // ----------------------------------------------------------------------------
+constexpr int CT_ROWS = 32;   // TOA rows per contraction tile (8 MFMA k-steps); T_aug is padded by this many zero rows
+
 struct PsrDev {
   int n_toa, m, ld, nb;      // varying layout: T_aug is n_toa x ld, r at ld-1
   int n_epoch;
@@ -180,6 +182,7 @@ struct PsrDev {
   const int* col_bgroup;     // ld entries, -1 = fixed column
   const double* ln_chrom;    // n_toa: ln(1400 / nu)
   const ewh_pref* bgroup;    // n_bgroup: chromatic index per group
+  const int* toa_ep;         // n_toa + CT_ROWS: 2 e + (last TOA of e), -1 = no epoch (pad rows -1)
 };
 
 // One factorisation job: (pulsar, sample) -> matrix + diagonal update.
@@ -261,8 +264,6 @@ __global__ __launch_bounds__(256) void epoch_sums_kernel(PsrDev P, const double*
 // output blocks are dealt round-robin to the waves; 32-row TOA tiles are
 // staged in LDS and shared by the four waves.
 // ----------------------------------------------------------------------------
-constexpr int CT_ROWS = 32;
-
 template <int NB>
 __global__ __launch_bounds__(256) void contract_mfma_kernel(PsrDev P, const double* __restrict__ w,
                                                             const double* __restrict__ beta,
@@ -346,6 +347,180 @@ __global__ __launch_bounds__(256) void contract_mfma_kernel(PsrDev P, const doub
       out[(long long)row * LD + col] = v;
       out[(long long)col * LD + row] = v;
     }
+  }
+}
+
+// ----------------------------------------------------------------------------
+// fp64 MFMA contraction, pipelined (default for pulsars without theta-dependent
+// basis columns).  One 256-thread workgroup (4 waves) per sample:
+//   G = T_aug^T W T_aug - sum_e beta_e s_e s_e^T,  s_e = sum_{t in e} w_t T_aug[t].
+//  * TOA tiles of CT_ROWS rows are copied global -> LDS by global_load_lds
+//    (16 B per lane, 1 KiB per wave-instruction; T_aug is contiguous and padded
+//    by CT_ROWS zero rows) into two buffers: tile i+1 streams in while the
+//    MFMAs run on tile i.
+//  * Wave WAVE owns the upper blocks blk = WAVE + 4 sl (compile-time, so the
+//    operand set is known): per k-step it reads T[row][16 j + c] once per block
+//    column j it touches and forms w_row * T[row][16 i + c] once per block row i.
+//  * ECORR: the epoch sums s_e are accumulated from the same LDS tile (thread
+//    = column; epochs are contiguous TOA runs that may straddle tiles) and
+//    written to a per-sample scratch; a second pass runs them through the same
+//    MFMA loop with weights -beta_e.  No second read of T from HBM.
+// ----------------------------------------------------------------------------
+typedef __attribute__((address_space(3))) void lds_void_t;
+typedef __attribute__((address_space(1))) void gbl_void_t;
+
+// block index blk of the upper triangle (row-major over i <= j) -> (i, j)
+constexpr int tri_i(int nb, int blk) {
+  int i = 0;
+  while (blk >= nb - i) { blk -= nb - i; ++i; }
+  return i;
+}
+constexpr int tri_j(int nb, int blk) {
+  int i = 0;
+  while (blk >= nb - i) { blk -= nb - i; ++i; }
+  return i + blk;
+}
+// does wave `wave` (blocks wave + 4 sl) touch block column j as a row (A) / at all?
+constexpr bool wave_uses_row(int nb, int wave, int j) {
+  for (int blk = wave; blk < nb * (nb + 1) / 2; blk += 4)
+    if (tri_i(nb, blk) == j) return true;
+  return false;
+}
+constexpr bool wave_uses(int nb, int wave, int j) {
+  for (int blk = wave; blk < nb * (nb + 1) / 2; blk += 4)
+    if (tri_i(nb, blk) == j || tri_j(nb, blk) == j) return true;
+  return false;
+}
+
+template <int NB, int WAVE>
+__device__ __forceinline__ void contract2_body(const PsrDev& P, const double* __restrict__ wrow,
+                                               const double* __restrict__ brow, double* __restrict__ srow,
+                                               double* __restrict__ Gout) {
+  extern __shared__ __attribute__((aligned(16))) double smem[];
+  constexpr int LD = 16 * NB;
+  constexpr int NBLK = NB * (NB + 1) / 2;
+  constexpr int SLOTS = (NBLK - WAVE + 3) / 4;
+  constexpr int TILE = CT_ROWS * LD;                 // doubles per tile
+  constexpr int CHUNKS = TILE * 8 / 1024 / 4;        // 1-KiB glds pieces per wave per tile (= NB)
+  static_assert(CHUNKS * 4 * 1024 == TILE * 8, "tile must split into 4 x NB pieces of 1 KiB");
+  // LDS: [2][TILE] tiles | [2][CT_ROWS] weights | [2][CT_ROWS] int epoch flags
+  const int tid = threadIdx.x, lane = tid & 63, q = lane >> 4, c = lane & 15;
+  double* const wbase = smem + 2 * TILE;
+  int* const ebase = (int*)(smem + 2 * TILE + 2 * CT_ROWS);
+
+  v4d acc[SLOTS > 0 ? SLOTS : 1];
+#pragma unroll
+  for (int sl = 0; sl < SLOTS; ++sl) acc[sl] = v4d{0.0, 0.0, 0.0, 0.0};
+
+  const bool ecorr = P.n_epoch > 0;
+  double eacc = 0.0;                                 // running s_e of column `tid`
+  // pass 0: TOA rows (weights w); pass 1: epoch rows (weights -beta)
+  for (int pass = 0; pass < (ecorr ? 2 : 1); ++pass) {
+    const int nrows = pass == 0 ? P.n_toa : P.n_epoch;
+    const double* src = pass == 0 ? P.T : srow;
+    const double* wsrc = pass == 0 ? wrow : brow;
+    const double wsign = pass == 0 ? 1.0 : -1.0;
+    const int ntile = (nrows + CT_ROWS - 1) / CT_ROWS;
+    auto issue = [&](int it) {
+      const char* g = (const char*)(src + (long long)it * TILE) + (WAVE * CHUNKS) * 1024 + lane * 16;
+      char* l = (char*)(smem + (it & 1) * TILE) + (WAVE * CHUNKS) * 1024;
+#pragma unroll
+      for (int k = 0; k < CHUNKS; ++k)
+        __builtin_amdgcn_global_load_lds((gbl_void_t*)(g + k * 1024), (lds_void_t*)(l + k * 1024), 16, 0, 0);
+    };
+    double wv = 0.0;
+    int ev = -1;
+    auto small = [&](int it) {
+      const int t = it * CT_ROWS + tid;
+      wv = (tid < CT_ROWS && t < nrows) ? wsign * wsrc[t] : 0.0;
+      ev = (pass == 0 && tid < CT_ROWS) ? P.toa_ep[t] : -1;
+    };
+    issue(0);
+    small(0);
+    if (tid < CT_ROWS) {
+      wbase[tid] = wv;
+      ebase[tid] = ev;
+    }
+    __syncthreads();
+    for (int it = 0; it < ntile; ++it) {
+      const int cur = it & 1;
+      if (it + 1 < ntile) {
+        issue(it + 1);
+        small(it + 1);
+      }
+      const double* tile = smem + cur * TILE;
+      const double* wt = wbase + cur * CT_ROWS;
+#pragma unroll
+      for (int kk = 0; kk < CT_ROWS / 4; ++kk) {
+        const int row = 4 * kk + q;
+        const double wr = wt[row];
+        const double* trow = tile + row * LD + c;
+        double tv[NB], av[NB];
+        static_for<0, NB>([&](auto J) {
+          constexpr int j = decltype(J)::value;
+          if constexpr (wave_uses(NB, WAVE, j)) tv[j] = trow[16 * j];
+          if constexpr (wave_uses_row(NB, WAVE, j)) av[j] = wr * tv[j];
+        });
+        static_for<0, SLOTS>([&](auto SL) {
+          constexpr int blk = WAVE + 4 * decltype(SL)::value;
+          constexpr int bi = tri_i(NB, blk), bj = tri_j(NB, blk);
+          acc[decltype(SL)::value] = __builtin_amdgcn_mfma_f64_16x16x4f64(av[bi], tv[bj], acc[decltype(SL)::value], 0, 0, 0);
+        });
+      }
+      if (pass == 0 && ecorr && tid < LD) {          // epoch sums of column tid
+        const double* tcol = tile + tid;
+        const int* ecur = ebase + cur * CT_ROWS;
+        for (int r = 0; r < CT_ROWS; ++r) {
+          const int e = ecur[r];
+          if (e >= 0) {
+            eacc = fma(wt[r], tcol[r * LD], eacc);
+            if (e & 1) {
+              srow[(long long)(e >> 1) * LD + tid] = eacc;
+              eacc = 0.0;
+            }
+          }
+        }
+      }
+      if (it + 1 < ntile && tid < CT_ROWS) {
+        wbase[(cur ^ 1) * CT_ROWS + tid] = wv;
+        ebase[(cur ^ 1) * CT_ROWS + tid] = ev;
+      }
+      __syncthreads();                               // drains the glds of tile it+1 (vmcnt(0))
+    }
+    if (pass == 0 && ecorr) __threadfence_block();   // s_e rows visible to the epoch pass
+    __syncthreads();
+  }
+  // epilogue: C/D layout lane -> (row q + 4r, col c); mirror to the lower half,
+  // unit diagonal on pad columns (m .. LD-2) so they factor as identity.
+  static_for<0, SLOTS>([&](auto SL) {
+    constexpr int blk = WAVE + 4 * decltype(SL)::value;
+    constexpr int bi = tri_i(NB, blk), bj = tri_j(NB, blk);
+#pragma unroll
+    for (int r = 0; r < 4; ++r) {
+      const int row = 16 * bi + q + 4 * r, col = 16 * bj + c;
+      double v = acc[decltype(SL)::value][r];
+      if (row == col && row >= P.m && row < LD - 1) v = 1.0;
+      Gout[(long long)row * LD + col] = v;
+      Gout[(long long)col * LD + row] = v;
+    }
+  });
+}
+
+template <int NB>
+__global__ __launch_bounds__(256) void contract2_kernel(PsrDev P, const double* __restrict__ w,
+                                                        const double* __restrict__ beta, double* __restrict__ s,
+                                                        long long s_stride, double* __restrict__ G) {
+  constexpr int LD = 16 * NB;
+  const int bl = blockIdx.x;
+  const double* wrow = w + (long long)bl * P.n_toa;
+  const double* brow = beta + (long long)bl * P.n_epoch;
+  double* srow = s + (long long)bl * s_stride;
+  double* Gout = G + (long long)bl * LD * LD;
+  switch (threadIdx.x >> 6) {
+    case 0: contract2_body<NB, 0>(P, wrow, brow, srow, Gout); break;
+    case 1: contract2_body<NB, 1>(P, wrow, brow, srow, Gout); break;
+    case 2: contract2_body<NB, 2>(P, wrow, brow, srow, Gout); break;
+    default: contract2_body<NB, 3>(P, wrow, brow, srow, Gout); break;
   }
 }
 
@@ -807,6 +982,7 @@ struct ewh_handle {
   size_t io_cap = 0;
   // varying-WN scratch
   double *d_w = nullptr, *d_beta = nullptr, *d_s = nullptr, *d_G = nullptr, *d_Kb = nullptr, *d_fac = nullptr;
+  long long s_stride = 0;     // doubles per sample in d_s (epoch rows padded to whole tiles)
   int chunk = 0;
   int last_B = 0;
 };
@@ -948,6 +1124,43 @@ int dispatch_contract(int nb, const PsrDev& P, const double* w, const double* be
   return 0;
 }
 
+constexpr int CONTRACT2_NB_MAX = 13;
+
+template <int NB>
+int launch_contract2(const PsrDev& P, const double* w, const double* beta, double* s, long long s_stride, double* G,
+                     int nb_samples, hipStream_t st) {
+  const size_t lds = (size_t)(2 * CT_ROWS * 16 * NB + 3 * CT_ROWS) * sizeof(double);
+  static bool attr = false;
+  if (!attr) {
+    EWH_HIP(hipFuncSetAttribute((const void*)contract2_kernel<NB>, hipFuncAttributeMaxDynamicSharedMemorySize,
+                                (int)lds));
+    attr = true;
+  }
+  hipLaunchKernelGGL(HIP_KERNEL_NAME(contract2_kernel<NB>), dim3(nb_samples), dim3(256), lds, st, P, w, beta, s,
+                     s_stride, G);
+  return 0;
+}
+
+int dispatch_contract2(int nb, const PsrDev& P, const double* w, const double* beta, double* s, long long s_stride,
+                       double* G, int nb_samples, hipStream_t st) {
+  switch (nb) {
+    case 1: return launch_contract2<1>(P, w, beta, s, s_stride, G, nb_samples, st);
+    case 2: return launch_contract2<2>(P, w, beta, s, s_stride, G, nb_samples, st);
+    case 3: return launch_contract2<3>(P, w, beta, s, s_stride, G, nb_samples, st);
+    case 4: return launch_contract2<4>(P, w, beta, s, s_stride, G, nb_samples, st);
+    case 5: return launch_contract2<5>(P, w, beta, s, s_stride, G, nb_samples, st);
+    case 6: return launch_contract2<6>(P, w, beta, s, s_stride, G, nb_samples, st);
+    case 7: return launch_contract2<7>(P, w, beta, s, s_stride, G, nb_samples, st);
+    case 8: return launch_contract2<8>(P, w, beta, s, s_stride, G, nb_samples, st);
+    case 9: return launch_contract2<9>(P, w, beta, s, s_stride, G, nb_samples, st);
+    case 10: return launch_contract2<10>(P, w, beta, s, s_stride, G, nb_samples, st);
+    case 11: return launch_contract2<11>(P, w, beta, s, s_stride, G, nb_samples, st);
+    case 12: return launch_contract2<12>(P, w, beta, s, s_stride, G, nb_samples, st);
+    case 13: return launch_contract2<13>(P, w, beta, s, s_stride, G, nb_samples, st);
+    default: return set_err(EWH_E_UNSUPPORTED, "basis too wide for the contraction kernel (> 207 columns)");
+  }
+}
+
 constexpr int default_waves(int nb) { return nb <= 8 ? 2 : 1; }
 
 template <int NB, int FULL = 0, int W = default_waves(NB), int ALG = 0>
@@ -1036,13 +1249,18 @@ int ensure_var_scratch(ewh_handle* h, int B) {
     maxfac = std::max(maxfac, (size_t)ps.n_toa * ps.dev.n_bgroup);
   }
   // chunk: keep G (ld^2) and s (E*ld) scratch under ~1.5 GB
-  const size_t per = (maxld * maxld + maxe * maxld + maxn + maxe + maxfac + 1) * sizeof(double);
+  // epoch-sum rows per sample: whole CT_ROWS tiles (+1) so the pipelined
+  // contraction's last epoch tile reads zero-initialised pad rows
+  const size_t sstride = ((maxe + CT_ROWS - 1) / CT_ROWS + 1) * CT_ROWS * maxld;
+  const size_t per = (maxld * maxld + sstride + maxn + maxe + maxfac + 1) * sizeof(double);
   size_t chunk = std::max<size_t>(1, (size_t)1536 * 1024 * 1024 / per);
   chunk = std::min<size_t>(chunk, std::min<size_t>(std::max(B, 1), 1024));
   int rc;
   if ((rc = dalloc(h, &h->d_w, chunk * maxn))) return rc;
   if ((rc = dalloc(h, &h->d_beta, chunk * maxe))) return rc;
-  if ((rc = dalloc(h, &h->d_s, chunk * maxe * maxld))) return rc;
+  if ((rc = dalloc(h, &h->d_s, chunk * sstride))) return rc;
+  EWH_HIP(hipMemset(h->d_s, 0, chunk * sstride * sizeof(double)));
+  h->s_stride = (long long)sstride;
   if ((rc = dalloc(h, &h->d_G, chunk * maxld * maxld))) return rc;
   if ((rc = dalloc(h, &h->d_Kb, chunk))) return rc;
   if ((rc = dalloc(h, &h->d_fac, chunk * maxfac))) return rc;
@@ -1061,6 +1279,12 @@ int run_white(ewh_handle* h, int p, const double* theta, int ldth, int b0, int n
   PsrHost& ps = h->psr[p];
   hipLaunchKernelGGL(wn_weights_kernel, dim3(nb), dim3(256), 0, h->stream, ps.dev, theta, ldth, b0, h->d_w,
                      h->d_beta, h->d_Kb, h->d_fac);
+  if (ps.dev.n_bgroup == 0 && h->kernel_mode != 7 && ps.nb <= CONTRACT2_NB_MAX) {
+    int rc = dispatch_contract2(ps.nb, ps.dev, h->d_w, h->d_beta, h->d_s, h->s_stride, h->d_G, nb, h->stream);
+    if (rc) return rc;
+    EWH_HIP(hipGetLastError());
+    return 0;
+  }
   if (ps.n_epoch > 0)
     hipLaunchKernelGGL(epoch_sums_kernel, dim3(ps.n_epoch, nb), dim3(256), 0, h->stream, ps.dev, h->d_w, h->d_fac,
                        h->d_s);
@@ -1155,7 +1379,8 @@ int ewh_create(const ewh_pta_desc* d, int device, ewh_handle** out) {
     for (int i = 0; i < s.n_slot; ++i) ps.has_theta_white |= pref_uses_theta(s.slots[i]);
     any_theta_white |= ps.has_theta_white || s.n_bgroup > 0;
     // T_aug: [basis | 0-pad | r], row-major n x ld
-    std::vector<double> Ta((size_t)s.n_toa * ps.ld, 0.0), sig2(s.n_toa);
+    // (+CT_ROWS zero rows: the pipelined contraction copies whole tiles)
+    std::vector<double> Ta((size_t)(s.n_toa + CT_ROWS) * ps.ld, 0.0), sig2(s.n_toa);
     for (int t = 0; t < s.n_toa; ++t) {
       for (int j = 0; j < s.n_col; ++j) Ta[(size_t)t * ps.ld + j] = s.basis[(size_t)t * s.n_col + j];
       Ta[(size_t)t * ps.ld + ps.ld - 1] = s.resid[t];
@@ -1173,6 +1398,11 @@ int ewh_create(const ewh_pta_desc* d, int device, ewh_handle** out) {
     if ((rc = dupload(h, &d_es, s.epoch_start, (size_t)s.n_epoch))) return bail(rc);
     if ((rc = dupload(h, &d_ee, s.epoch_stop, (size_t)s.n_epoch))) return bail(rc);
     if ((rc = dupload(h, &d_eslot, s.epoch_slot, (size_t)s.n_epoch))) return bail(rc);
+    std::vector<int> toa_ep((size_t)s.n_toa + CT_ROWS, -1);
+    for (int e = 0; e < s.n_epoch; ++e)
+      for (int t = s.epoch_start[e]; t < s.epoch_stop[e]; ++t) toa_ep[t] = 2 * e + (t == s.epoch_stop[e] - 1);
+    int* d_tep;
+    if ((rc = dupload(h, &d_tep, toa_ep.data(), toa_ep.size()))) return bail(rc);
     int* d_cbg = nullptr;
     double* d_lnc = nullptr;
     ewh_pref* d_bg = nullptr;
@@ -1184,7 +1414,7 @@ int ewh_create(const ewh_pta_desc* d, int device, ewh_handle** out) {
       if ((rc = dupload(h, &d_bg, s.bgroup_idx, (size_t)s.n_bgroup))) return bail(rc);
     }
     ps.dev = PsrDev{s.n_toa, s.n_col, ps.ld, ps.nb, s.n_epoch, dT, dsig2, d_ef, d_eq, d_slots, d_es, d_ee, d_eslot,
-                    s.n_bgroup, d_cbg, d_lnc, d_bg};
+                    s.n_bgroup, d_cbg, d_lnc, d_bg, d_tep};
     std::vector<int> ptr;
     std::vector<DSpec> ent;
     build_csr(s, 0, s.n_col, ptr, ent);
@@ -1205,7 +1435,7 @@ int ewh_create(const ewh_pta_desc* d, int device, ewh_handle** out) {
 }
 
 int ewh_set_kernel_mode(ewh_handle* h, int32_t mode) {
-  if (!h || mode < 0 || mode > 6) return set_err(EWH_E_INVALID, "bad handle / mode");
+  if (!h || mode < 0 || mode > 7) return set_err(EWH_E_INVALID, "bad handle / mode");
   h->kernel_mode = mode;
   return 0;
 }

@@ -156,7 +156,9 @@ double ewh_unit_cost(const ewh_handle* h, int32_t pulsar);
  * the LDS kernel, 2 = the round-1 MFMA kernel (Cholesky panel, looped steps).
  * A/B variants for NB = 8 only (else as 0): 3 = LDL^T at one wave per SIMD,
  * 4 = LDL^T with looped steps, 5 = Cholesky panel with unrolled steps,
- * 6 = LDL^T with the row broadcast through LDS. */
+ * 6 = LDL^T with the row broadcast through LDS.  7 = default Cholesky with
+ * the round-1 contraction (varying white noise: separate epoch-sum kernel,
+ * unpipelined tiles) instead of the pipelined one. */
 int ewh_set_kernel_mode(ewh_handle* h, int32_t mode);
 
 void ewh_destroy(ewh_handle* h);

@@ -35,6 +35,7 @@ def main():
     ap.add_argument("--configs", default="c2,c3,c4")
     ap.add_argument("--reps", type=int, default=3)
     ap.add_argument("--check", type=int, default=3)
+    ap.add_argument("--mode", type=int, default=0, help="ewh_set_kernel_mode (7: round-1 contraction)")
     args = ap.parse_args()
     import torch
     from enterprise_warp_amd import synth
@@ -47,6 +48,7 @@ def main():
         X = synth.near_draws(pta, cfg.truth, B, 11)
         t0 = time.time()
         eng = pta.engine(0)
+        eng.set_kernel_mode(args.mode)
         create_s = time.time() - t0
         th = torch.from_numpy(X).cuda()
         out = torch.zeros(B, dtype=torch.float64, device="cuda")
@@ -65,7 +67,7 @@ def main():
         idx = np.arange(min(args.check, B))
         want = oracle_vals(pta, X[idx])
         tol = 1e-6 + 1e-10 * np.abs(want)
-        rec = {"config": name, "n_pulsars": len(pta.signal_collections), "B": B,
+        rec = {"config": name, "mode": args.mode, "n_pulsars": len(pta.signal_collections), "B": B,
                "basis": sorted({c.T.shape[1] for c in pta.signal_collections}),
                "white_fixed": pta.white_fixed(), "ms_per_batch": float(np.median(ts)),
                "evals_per_s": B / (np.median(ts) * 1e-3), "host_build_s": build_s, "engine_create_s": create_s,
