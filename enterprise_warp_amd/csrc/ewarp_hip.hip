@@ -690,6 +690,102 @@ __device__ __forceinline__ void syrk_update(v4d& C, const v4d& Ui, const v4d& Uj
 // (one vector rsqrt per register instead of one serial rsqrt per pivot).  The
 // per-pivot dependency chain drops the scale -> ds_bpermute leg; log|Sigma| =
 // sum log d_k is accumulated per block row from the lanes' own pivots.
+// LDL^T panel of block row BB over the blocks blk(j), j = BB..NB-1 (C/D
+// layout, upper triangle), used by the register-resident kernels: the 16
+// pivots are factored by VALU (ALG 1: row k broadcast by ds_bpermute, ALG 2:
+// through the per-wave LDS `rowbuf`), then the block row is scaled to
+// U = D^-1/2 V.  Accumulates log d_k (one lane per row) and d_k > 0 per lane.
+template <int NB, int FULL, int ALG, typename BBt, typename Blk>
+__device__ __forceinline__ void panel_ldl_row(BBt BBc, Blk&& blk, int q, int c, LogAcc& ldet, bool& ok,
+                                              double* rowbuf) {
+  constexpr int LD = 16 * NB;
+  (void)rowbuf;
+  (void)LD;
+  constexpr int bb = decltype(BBc)::value;
+  static_for<0, 4>([&](auto KR) {
+    constexpr int kr = decltype(KR)::value;
+    auto step = [&](const int kq) {
+      const int k = 4 * kr + kq;
+      const double d = readlane_d(blk(BBc)[kr], 16 * kq + k);            // wave-uniform pivot
+      // raw row k: A[k][q + 4r] for this lane's rows (masked to rows > k) and
+      // A[k][col c] of every block of the row; both in flight while 1/d forms
+      double ui[4];
+      double rk[NB];
+      if constexpr (ALG == 2) {
+        // LDS broadcast: the 16 lanes of quad kq store row k of every block
+        // (one ds_write_b64 per block), every lane reads it back with 16
+        // distinct addresses per read (broadcast, bank-conflict free) --
+        // several times cheaper on the CU's LDS than two ds_bpermute_b32
+        // per double.  One wave per workgroup and LDS ops of a wave run in
+        // order, so no barrier: the asm fences only stop the compiler from
+        // moving the reads above the other lanes' writes.
+        double* rb = rowbuf + (k & 1) * LD;
+        if (q == kq) {
+          static_for<bb, NB>([&](auto JJ) {
+            constexpr int j = decltype(JJ)::value;
+            rb[16 * j + c] = blk(JJ)[kr];
+          });
+        }
+        asm volatile("" ::: "memory");
+        static_for<kr, 4>([&](auto R) {
+          constexpr int r = decltype(R)::value;
+          const double v = rb[16 * bb + q + 4 * r];
+          ui[r] = (r > kr || q > kq) ? v : 0.0;
+        });
+        static_for<bb, NB>([&](auto JJ) {
+          constexpr int j = decltype(JJ)::value;
+          rk[j] = rb[16 * j + c];
+        });
+        asm volatile("" ::: "memory");
+      } else {
+        static_for<kr, 4>([&](auto R) {
+          constexpr int r = decltype(R)::value;
+          const double v = __shfl(blk(BBc)[kr], 16 * kq + q + 4 * r);
+          ui[r] = (r > kr || q > kq) ? v : 0.0;
+        });
+        static_for<bb, NB>([&](auto JJ) {
+          constexpr int j = decltype(JJ)::value;
+          rk[j] = __shfl(blk(JJ)[kr], 16 * kq + c);
+        });
+      }
+      const double dinv = rcp_nr(d);
+      static_for<kr, 4>([&](auto R) { ui[decltype(R)::value] *= dinv; });
+      static_for<bb, NB>([&](auto JJ) {
+        constexpr int j = decltype(JJ)::value;
+        static_for<kr, 4>([&](auto R) {
+          constexpr int r = decltype(R)::value;
+          blk(JJ)[r] = fma(-ui[r], rk[j], blk(JJ)[r]);
+        });
+      });
+    };
+    constexpr int nk = (bb == NB - 1 && kr == 3) ? 3 : 4;   // the r column is not pivoted
+    if constexpr (FULL) {
+      static_for<0, nk>([&](auto KQ) {
+        step(decltype(KQ)::value);
+        // unrolled LDS-broadcast steps: keep the scheduler from hoisting the
+        // next steps' LDS reads (it otherwise spills ~1 KB per lane)
+        if constexpr (ALG == 2) __builtin_amdgcn_sched_barrier(0);
+      });
+    } else {
+#pragma unroll 1
+      for (int kq = 0; kq < nk; ++kq) step(kq);
+    }
+  });
+  // rows of the block row -> U = d^-1/2 V, d of row q + 4r read from the
+  // diagonal (lane 17q + 4r); log-det and positivity from one lane per row
+  // (c == 0); the r row (last block, row 15) is left as it is
+  static_for<0, 4>([&](auto R) {
+    constexpr int r = decltype(R)::value;
+    const bool rrow = (bb == NB - 1 && r == 3) && q == 3;
+    const double dg = __shfl(blk(BBc)[r], 17 * q + 4 * r);
+    const double dv = rrow ? 1.0 : dg;
+    ok = ok && (dv > 0.0);
+    if (c == 0) ldet.add(dv);
+    const double rs = rrow ? 1.0 : rsqrt_nr(dv);
+    static_for<bb, NB>([&](auto JJ) { blk(JJ)[r] *= rs; });
+  });
+}
+
 template <int NB, int FULL, int W, int ALG = 0>
 __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(W, W)))
 void chol_mfma_kernel(const CholJob* __restrict__ jobs, int B, long long u0, int b_off,
@@ -740,89 +836,7 @@ void chol_mfma_kernel(const CholJob* __restrict__ jobs, int B, long long u0, int
   bool ok = true;
   // LDL^T panel row bb (ALG >= 1)
   auto panel_ldl = [&](auto BBc, auto&& blk) {
-    constexpr int bb = decltype(BBc)::value;
-    static_for<0, 4>([&](auto KR) {
-      constexpr int kr = decltype(KR)::value;
-      auto step = [&](const int kq) {
-        const int k = 4 * kr + kq;
-        const double d = readlane_d(blk(BBc)[kr], 16 * kq + k);            // wave-uniform pivot
-        // raw row k: A[k][q + 4r] for this lane's rows (masked to rows > k) and
-        // A[k][col c] of every block of the row; both in flight while 1/d forms
-        double ui[4];
-        double rk[NB];
-        if constexpr (ALG == 2) {
-          // LDS broadcast: the 16 lanes of quad kq store row k of every block
-          // (one ds_write_b64 per block), every lane reads it back with 16
-          // distinct addresses per read (broadcast, bank-conflict free) --
-          // several times cheaper on the CU's LDS than two ds_bpermute_b32
-          // per double.  One wave per workgroup and LDS ops of a wave run in
-          // order, so no barrier: the asm fences only stop the compiler from
-          // moving the reads above the other lanes' writes.
-          double* rb = rowbuf + (k & 1) * LD;
-          if (q == kq) {
-            static_for<bb, NB>([&](auto JJ) {
-              constexpr int j = decltype(JJ)::value;
-              rb[16 * j + c] = blk(JJ)[kr];
-            });
-          }
-          asm volatile("" ::: "memory");
-          static_for<kr, 4>([&](auto R) {
-            constexpr int r = decltype(R)::value;
-            const double v = rb[16 * bb + q + 4 * r];
-            ui[r] = (r > kr || q > kq) ? v : 0.0;
-          });
-          static_for<bb, NB>([&](auto JJ) {
-            constexpr int j = decltype(JJ)::value;
-            rk[j] = rb[16 * j + c];
-          });
-          asm volatile("" ::: "memory");
-        } else {
-          static_for<kr, 4>([&](auto R) {
-            constexpr int r = decltype(R)::value;
-            const double v = __shfl(blk(BBc)[kr], 16 * kq + q + 4 * r);
-            ui[r] = (r > kr || q > kq) ? v : 0.0;
-          });
-          static_for<bb, NB>([&](auto JJ) {
-            constexpr int j = decltype(JJ)::value;
-            rk[j] = __shfl(blk(JJ)[kr], 16 * kq + c);
-          });
-        }
-        const double dinv = rcp_nr(d);
-        static_for<kr, 4>([&](auto R) { ui[decltype(R)::value] *= dinv; });
-        static_for<bb, NB>([&](auto JJ) {
-          constexpr int j = decltype(JJ)::value;
-          static_for<kr, 4>([&](auto R) {
-            constexpr int r = decltype(R)::value;
-            blk(JJ)[r] = fma(-ui[r], rk[j], blk(JJ)[r]);
-          });
-        });
-      };
-      constexpr int nk = (bb == NB - 1 && kr == 3) ? 3 : 4;   // the r column is not pivoted
-      if constexpr (FULL) {
-        static_for<0, nk>([&](auto KQ) {
-          step(decltype(KQ)::value);
-          // unrolled LDS-broadcast steps: keep the scheduler from hoisting the
-          // next steps' LDS reads (it otherwise spills ~1 KB per lane)
-          if constexpr (ALG == 2) __builtin_amdgcn_sched_barrier(0);
-        });
-      } else {
-#pragma unroll 1
-        for (int kq = 0; kq < nk; ++kq) step(kq);
-      }
-    });
-    // rows of the block row -> U = d^-1/2 V, d of row q + 4r read from the
-    // diagonal (lane 17q + 4r); log-det and positivity from one lane per row
-    // (c == 0); the r row (last block, row 15) is left as it is
-    static_for<0, 4>([&](auto R) {
-      constexpr int r = decltype(R)::value;
-      const bool rrow = (bb == NB - 1 && r == 3) && q == 3;
-      const double dg = __shfl(blk(BBc)[r], 17 * q + 4 * r);
-      const double dv = rrow ? 1.0 : dg;
-      ok = ok && (dv > 0.0);
-      if (c == 0) ldet.add(dv);
-      const double rs = rrow ? 1.0 : rsqrt_nr(dv);
-      static_for<bb, NB>([&](auto JJ) { blk(JJ)[r] *= rs; });
-    });
+    panel_ldl_row<NB, FULL, ALG>(BBc, blk, q, c, ldet, ok, rowbuf);
   };
   // panel row bb over the blocks blk(j), j = bb..NB-1
   auto panel = [&](auto BBc, auto&& blk) {
@@ -933,6 +947,106 @@ void chol_mfma_kernel(const CholJob* __restrict__ jobs, int B, long long u0, int
   }
 }
 
+// ----------------------------------------------------------------------------
+// batched factorisation for wide bases (NB > 9, e.g. C4's 193-wide Sigma):
+// one wave per unit, LEFT-looking over block rows.  Block row i (<= NB
+// blocks, C/D layout) is loaded into registers, takes the updates
+// A_ij -= U_pi^T U_pj of every finished row p < i (4 MFMAs per block, the U
+// blocks streamed back from a per-wave scratch in the same lane layout,
+// double-buffered), is factored by the LDL^T panel and written to scratch.
+// Same arithmetic as chol_mfma_kernel (right-looking), re-ordered.
+// ----------------------------------------------------------------------------
+constexpr int BIG_NB_MAX = 16;
+
+template <int NB>
+__device__ __forceinline__ long long big_blk(int p, int j) {   // packed upper block index
+  return (long long)p * NB - (long long)p * (p - 1) / 2 + (j - p);
+}
+
+template <int NB>
+__global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(1, 1)))
+void chol_big_kernel(const CholJob* __restrict__ jobs, int B, long long u0, int b_off,
+                     const double* __restrict__ theta, int ldth, double* __restrict__ out_units,
+                     double* __restrict__ scratch) {
+  constexpr int LD = 16 * NB;
+  __shared__ double phinv[LD];
+  const int lane = threadIdx.x;
+  const int q = lane >> 4, c = lane & 15;
+  const long long u = u0 + blockIdx.x;
+  const int p = (int)(u / B), b = (int)(u % B);
+  const CholJob J = jobs[p];
+  const double* A = J.mats + (long long)(b - b_off) * J.mstride;
+  const double* th = theta + (long long)b * ldth;
+  double* scr = scratch + (long long)blockIdx.x * (NB * (NB + 1) / 2) * 256 + lane * 4;
+
+  LogAcc lphi;
+  for (int a = lane; a < LD; a += 64) {
+    double pi = 0.0;
+    if (a < J.mreal) {
+      double ph = 0.0;
+      for (int e = J.col_ptr[a]; e < J.col_ptr[a + 1]; ++e) ph += spec_phi(J.spec[e], th);
+      pi = 1.0 / ph;
+      lphi.add(ph);
+    }
+    phinv[a] = pi;
+  }
+  const double lphi_sum = wave_sum(lphi.value());
+  __syncthreads();
+
+  LogAcc ldet;
+  bool ok = true;
+  double qv = 0.0;
+  static_for<0, NB>([&](auto I) {
+    constexpr int i = decltype(I)::value;
+    constexpr int W = NB - i;                       // blocks in row i
+    v4d R[W];
+    static_for<0, W>([&](auto JJ) {
+      constexpr int j = i + decltype(JJ)::value;
+      static_for<0, 4>([&](auto RR) {
+        constexpr int r = decltype(RR)::value;
+        R[j - i][r] = A[(long long)(16 * i + q + 4 * r) * LD + 16 * j + c];
+      });
+      if constexpr (j == i) {
+        const double pd = phinv[16 * i + c];
+        static_for<0, 4>([&](auto RR) {
+          constexpr int r = decltype(RR)::value;
+          R[0][r] += (q + 4 * r == c) ? pd : 0.0;
+        });
+      }
+    });
+    if constexpr (i > 0) {
+      // U blocks (p, i..NB-1) of earlier rows: Ui once, then each Uj in turn
+      // (the compiler issues the row's loads ahead of its MFMAs)
+#pragma unroll 1
+      for (int pp = 0; pp < i; ++pp) {
+        const v4d Ui = *(const v4d*)(scr + big_blk<NB>(pp, i) * 256);
+        static_for<0, W>([&](auto JJ) {
+          constexpr int jj = decltype(JJ)::value;
+          const v4d Uj = *(const v4d*)(scr + big_blk<NB>(pp, i + jj) * 256);
+          syrk_update(R[jj], Ui, Uj);
+        });
+      }
+    }
+    panel_ldl_row<NB, 0, 1>(I, [&](auto JJ) -> v4d& { return R[decltype(JJ)::value - i]; }, q, c, ldet, ok,
+                            nullptr);
+    if constexpr (i < NB - 1) {
+      static_for<0, W>([&](auto JJ) {
+        constexpr int j = i + decltype(JJ)::value;
+        *(v4d*)(scr + big_blk<NB>(i, j) * 256) = R[j - i];
+      });
+    } else {
+      qv = readlane_d(R[0][3], 63);
+    }
+  });
+  const double ldet_v = wave_sum(ldet.value());
+  const bool ok_all = __all(ok);
+  if (lane == 0) {
+    double lnl = J.K[(long long)(b - b_off) * J.kstride] - 0.5 * qv - 0.5 * ldet_v - 0.5 * lphi_sum;
+    if (!ok_all || J.fail) lnl = -INFINITY;
+    out_units[(long long)p * B + b] = lnl;
+  }
+}
+
 // out[b] = sum_p units[p * B + b], pulsars in order.
 __global__ void reduce_units_kernel(const double* __restrict__ units, int P, int B, double* __restrict__ out) {
   const int b = blockIdx.x * blockDim.x + threadIdx.x;
@@ -983,6 +1097,9 @@ struct ewh_handle {
   // varying-WN scratch
   double *d_w = nullptr, *d_beta = nullptr, *d_s = nullptr, *d_G = nullptr, *d_Kb = nullptr, *d_fac = nullptr;
   long long s_stride = 0;     // doubles per sample in d_s (epoch rows padded to whole tiles)
+  double* d_bigscr = nullptr; // chol_big_kernel: per-workgroup U blocks
+  long long bigscr_cap = 0;   // workgroups per launch it holds
+  int bigscr_nb = 0;
   int chunk = 0;
   int last_B = 0;
 };
@@ -1170,9 +1287,30 @@ void launch_chol_mfma(const CholJob* jobs, int B, long long u0, long long n, int
                      u0, b_off, theta, ldth, units);
 }
 
+template <int NB>
+void launch_chol_big(const CholJob* jobs, int B, long long u0, long long n, int b_off, const double* theta, int ldth,
+                     double* units, double* scr, long long cap, hipStream_t st) {
+  for (long long o = 0; o < n; o += cap)   // one scratch slot per workgroup of a launch
+    hipLaunchKernelGGL(HIP_KERNEL_NAME(chol_big_kernel<NB>), dim3((unsigned)std::min(cap, n - o)), dim3(64), 0, st,
+                       jobs, B, u0 + o, b_off, theta, ldth, units, scr);
+}
+
 int dispatch_chol(int mode, int nb, int mreal, const CholJob* jobs, int B, long long u0, long long n, int b_off,
-                  const double* theta, int ldth, double* units, hipStream_t st) {
+                  const double* theta, int ldth, double* units, hipStream_t st, double* bigscr = nullptr,
+                  long long bigcap = 0) {
   if (n <= 0) return 0;
+  if (mode != 1 && nb > MFMA_NB_MAX && nb <= BIG_NB_MAX && bigscr) {
+    switch (nb) {
+      case 10: launch_chol_big<10>(jobs, B, u0, n, b_off, theta, ldth, units, bigscr, bigcap, st); return 0;
+      case 11: launch_chol_big<11>(jobs, B, u0, n, b_off, theta, ldth, units, bigscr, bigcap, st); return 0;
+      case 12: launch_chol_big<12>(jobs, B, u0, n, b_off, theta, ldth, units, bigscr, bigcap, st); return 0;
+      case 13: launch_chol_big<13>(jobs, B, u0, n, b_off, theta, ldth, units, bigscr, bigcap, st); return 0;
+      case 14: launch_chol_big<14>(jobs, B, u0, n, b_off, theta, ldth, units, bigscr, bigcap, st); return 0;
+      case 15: launch_chol_big<15>(jobs, B, u0, n, b_off, theta, ldth, units, bigscr, bigcap, st); return 0;
+      case 16: launch_chol_big<16>(jobs, B, u0, n, b_off, theta, ldth, units, bigscr, bigcap, st); return 0;
+      default: break;
+    }
+  }
   // A/B variants (NB = 8, the C3 reduced width); see ewh_set_kernel_mode
   if (nb == 8 && mode >= 3) {
     switch (mode) {
@@ -1215,6 +1353,22 @@ int dispatch_chol(int mode, int nb, int mreal, const CholJob* jobs, int B, long 
     attr_set = true;
   }
   hipLaunchKernelGGL(chol_lds_kernel, dim3((unsigned)n), dim3(256), lds, st, jobs, B, u0, b_off, theta, ldth, units);
+  return 0;
+}
+
+// scratch of chol_big_kernel for NB: BIG_SLOTS workgroups x NB(NB+1)/2 blocks of 2 KiB
+constexpr long long BIG_SLOTS = 2048;
+int ensure_big_scratch(ewh_handle* h, int nb) {
+  if (nb <= MFMA_NB_MAX || nb > BIG_NB_MAX || nb <= h->bigscr_nb) return 0;
+  if (h->d_bigscr) {
+    hipFree(h->d_bigscr);
+    h->allocs.erase(std::find(h->allocs.begin(), h->allocs.end(), (void*)h->d_bigscr));
+    h->d_bigscr = nullptr;
+  }
+  int rc = dalloc(h, &h->d_bigscr, (size_t)BIG_SLOTS * (nb * (nb + 1) / 2) * 256);
+  if (rc) return rc;
+  h->bigscr_cap = BIG_SLOTS;
+  h->bigscr_nb = nb;
   return 0;
 }
 
@@ -1472,8 +1626,9 @@ int ewh_lnl_units_device(ewh_handle* h, const double* theta_dev, int32_t B, int6
       const long long seg_end = std::min<long long>(u_end, (long long)p1 * B);
       int maxm = 0;
       for (int p = p0; p < p1; ++p) maxm = std::max(maxm, h->psr[p].fx_m);
-      if ((rc = dispatch_chol(h->kernel_mode, nb0, maxm, h->d_jobs_fixed, B, u, seg_end - u, 0, theta_dev, ldth,
-                              h->d_units, st))) {
+      if ((rc = ensure_big_scratch(h, nb0)) ||
+          (rc = dispatch_chol(h->kernel_mode, nb0, maxm, h->d_jobs_fixed, B, u, seg_end - u, 0, theta_dev, ldth,
+                              h->d_units, st, h->d_bigscr, h->bigscr_cap))) {
         h->stream = saved;
         return rc;
       }
@@ -1494,8 +1649,10 @@ int ewh_lnl_units_device(ewh_handle* h, const double* theta_dev, int32_t B, int6
           h->stream = saved;
           return rc;
         }
-        if ((rc = dispatch_chol(h->kernel_mode, h->psr[p].nb, h->psr[p].m, h->d_jobs_var, B,
-                                (long long)p * B + c0, nb, c0, theta_dev, ldth, h->d_units, st))) {
+        if ((rc = ensure_big_scratch(h, h->psr[p].nb)) ||
+            (rc = dispatch_chol(h->kernel_mode, h->psr[p].nb, h->psr[p].m, h->d_jobs_var, B,
+                                (long long)p * B + c0, nb, c0, theta_dev, ldth, h->d_units, st, h->d_bigscr,
+                                h->bigscr_cap))) {
           h->stream = saved;
           return rc;
         }

@@ -35,7 +35,7 @@ def test_golden_vectors(require_gpu, name):
     _check(got, lnl, min_eig, name)
 
 
-@pytest.mark.parametrize("name", ["c2_small", "c3_small"])
+@pytest.mark.parametrize("name", ["c2_small", "c3_small", "c4_small"])
 def test_lds_kernel_matches_mfma_kernel(require_gpu, name):
     pta, X, lnl, min_eig = load_golden(name)
     a = pta.get_lnlikelihood_batch(X)
