@@ -84,9 +84,13 @@ __device__ __forceinline__ double dpar(int idx, double cval, const double* th) {
 
 constexpr double LN10 = 2.302585092994045684;
 
-// __noinline__: ROCm 7.2 clang crashes in the CGSCC inliner when this is inlined into both
-// the schur and LDS-Cholesky kernels; it runs before the factorisation, so the call is cheap.
-__device__ __noinline__ double spec_phi(const DSpec& s, const double* th) {
+// spec_phi_body: the arithmetic; spec_phi: an out-of-line copy for the schur and
+// LDS-Cholesky kernels (ROCm 7.2 clang crashes in the CGSCC inliner when one
+// inlined copy serves both); the register-resident kernels inline the body
+// (a call there reserves a scratch frame the unrolled factorisation then
+// spills into).
+template <int DUMMY = 0>
+__device__ __forceinline__ double spec_phi_body(const DSpec& s, const double* th) {
   switch (s.kind) {
     case EWH_SPEC_POWERLAW: {
       const double lgA = dpar(s.i0, s.v0, th), gam = dpar(s.i1, s.v1, th);
@@ -106,6 +110,8 @@ __device__ __noinline__ double spec_phi(const DSpec& s, const double* th) {
       return __builtin_nan("");
   }
 }
+
+__device__ __noinline__ double spec_phi(const DSpec& s, const double* th) { return spec_phi_body(s, th); }
 
 // running log-determinant without a log per term: product of frexp mantissas
 // (each in [0.5, 1): >= 2^-1000 after 1000 terms, no underflow) + exponent sum.
@@ -133,6 +139,15 @@ __device__ __forceinline__ double rsqrt_nr(double a) {
   y = fma(y, t, y);
   t = fma(-h * y, y, 0.5);
   return fma(y, t, y);
+}
+
+// XCD-aware unit order: the dispatcher deals workgroup b to XCD b % 8, so
+// XCD x gets the contiguous unit range [x q, (x+1) q) (q = n / 8; the n % 8
+// tail maps to itself).  Units are pulsar-major, so each pulsar's reduced
+// matrix is fetched into ~one XCD's L2 instead of all eight.
+__device__ __forceinline__ long long xcd_unit(unsigned b, unsigned n) {
+  const unsigned q = n >> 3;
+  return b < (q << 3) ? (long long)(b & 7) * q + (b >> 3) : (long long)b;
 }
 
 // 1/a: hardware estimate + two Newton steps (~1 ulp).
@@ -655,7 +670,9 @@ __global__ __launch_bounds__(256) void chol_lds_kernel(const CholJob* __restrict
 // ----------------------------------------------------------------------------
 template <int NB>
 struct Split {
-  static constexpr int H = NB / 2;                    // block rows of phase 1
+  // block rows of phase 1: NB/2, except 3 of 8 (phase 1's 21 blocks + panel
+  // temporaries then fit 256 VGPRs without spills; phase 2 runs row by row)
+  static constexpr int H = NB == 8 ? 3 : NB / 2;
   static constexpr int M = NB - H;                    // A22 block order
   static constexpr int n1 = H * NB - H * (H - 1) / 2; // blocks (i < H, j >= i)
   static constexpr int n2 = M * (M + 1) / 2;          // blocks (H <= i <= j)
@@ -797,7 +814,7 @@ void chol_mfma_kernel(const CholJob* __restrict__ jobs, int B, long long u0, int
   __shared__ double rowbuf[ALG == 2 ? 2 * LD : 1];   // ALG 2: double-buffered row-k broadcast
   const int lane = threadIdx.x;
   const int q = lane >> 4, c = lane & 15;
-  const long long u = u0 + blockIdx.x;
+  const long long u = u0 + xcd_unit(blockIdx.x, gridDim.x);
   const int p = (int)(u / B), b = (int)(u % B);
   const CholJob J = jobs[p];
   const double* A = J.mats + (long long)(b - b_off) * J.mstride;
@@ -808,7 +825,7 @@ void chol_mfma_kernel(const CholJob* __restrict__ jobs, int B, long long u0, int
     double pi = 0.0;
     if (a < J.mreal) {
       double ph = 0.0;
-      for (int e = J.col_ptr[a]; e < J.col_ptr[a + 1]; ++e) ph += spec_phi(J.spec[e], th);
+      for (int e = J.col_ptr[a]; e < J.col_ptr[a + 1]; ++e) ph += spec_phi_body(J.spec[e], th);
       pi = 1.0 / ph;
       lphi.add(ph);
     }
@@ -906,17 +923,15 @@ void chol_mfma_kernel(const CholJob* __restrict__ jobs, int B, long long u0, int
     });
   });
   // ---- phase 2: A22 -= U12^T U12 ----
+  // block by block in row order: U1 column i is dead once row i of A22 is done
   v4d U2[S::n2];
-  static_for<H, NB>([&](auto BI) {
-    constexpr int bi = decltype(BI)::value;
-    static_for<bi, NB>([&](auto BJ) { load_block(BI, BJ, U2[S::i2(bi, decltype(BJ)::value)]); });
-  });
-  static_for<0, H>([&](auto BBc) {
-    constexpr int bb = decltype(BBc)::value;
-    static_for<H, NB>([&](auto II) {
-      constexpr int i = decltype(II)::value;
-      static_for<i, NB>([&](auto JJ) {
-        constexpr int j = decltype(JJ)::value;
+  static_for<H, NB>([&](auto II) {
+    constexpr int i = decltype(II)::value;
+    static_for<i, NB>([&](auto JJ) {
+      constexpr int j = decltype(JJ)::value;
+      load_block(II, JJ, U2[S::i2(i, j)]);
+      static_for<0, H>([&](auto BBc) {
+        constexpr int bb = decltype(BBc)::value;
         syrk_update(U2[S::i2(i, j)], U1[S::i1(bb, i)], U1[S::i1(bb, j)]);
       });
     });
@@ -972,7 +987,7 @@ void chol_big_kernel(const CholJob* __restrict__ jobs, int B, long long u0, int 
   __shared__ double phinv[LD];
   const int lane = threadIdx.x;
   const int q = lane >> 4, c = lane & 15;
-  const long long u = u0 + blockIdx.x;
+  const long long u = u0 + xcd_unit(blockIdx.x, gridDim.x);
   const int p = (int)(u / B), b = (int)(u % B);
   const CholJob J = jobs[p];
   const double* A = J.mats + (long long)(b - b_off) * J.mstride;
@@ -984,7 +999,7 @@ void chol_big_kernel(const CholJob* __restrict__ jobs, int B, long long u0, int 
     double pi = 0.0;
     if (a < J.mreal) {
       double ph = 0.0;
-      for (int e = J.col_ptr[a]; e < J.col_ptr[a + 1]; ++e) ph += spec_phi(J.spec[e], th);
+      for (int e = J.col_ptr[a]; e < J.col_ptr[a + 1]; ++e) ph += spec_phi_body(J.spec[e], th);
       pi = 1.0 / ph;
       lphi.add(ph);
     }
