@@ -10,7 +10,7 @@ import os
 _HERE = os.path.dirname(os.path.abspath(__file__))
 LIB_PATH = os.path.join(_HERE, "libewarp_hip.so")
 
-EWH_ABI_VERSION = 2
+EWH_ABI_VERSION = 3
 SPEC_POWERLAW, SPEC_TURNOVER, SPEC_FREESPEC, SPEC_CONST = 1, 2, 3, 4
 
 
@@ -34,12 +34,17 @@ class PulsarDesc(C.Structure):
                 ("efac_slot", _ip), ("equad_slot", _ip),
                 ("n_epoch", C.c_int32), ("epoch_start", _ip), ("epoch_stop", _ip), ("epoch_slot", _ip),
                 ("spec", C.POINTER(SpecEntry)),
-                ("n_bgroup", C.c_int32), ("bgroup_idx", C.POINTER(Pref)), ("col_bgroup", _ip), ("ln_chrom", _dp)]
+                ("n_bgroup", C.c_int32), ("bgroup_idx", C.POINTER(Pref)), ("col_bgroup", _ip), ("ln_chrom", _dp),
+                ("n_common", C.c_int32)]
+
+
+class CommonDesc(C.Structure):
+    _fields_ = [("n_col", C.c_int32), ("orf", _dp), ("spec", C.POINTER(SpecEntry))]
 
 
 class PtaDesc(C.Structure):
     _fields_ = [("abi_version", C.c_int32), ("n_pulsar", C.c_int32), ("n_param", C.c_int32),
-                ("white_fixed", C.c_int32), ("pulsars", C.POINTER(PulsarDesc))]
+                ("white_fixed", C.c_int32), ("pulsars", C.POINTER(PulsarDesc)), ("common", C.POINTER(CommonDesc))]
 
 
 EXPORTS = ["ewh_create", "ewh_lnl_batch", "ewh_lnl_units_device", "ewh_last_unit_terms", "ewh_unit_cost",

@@ -1,0 +1,53 @@
+// chol_small.hip — register-resident factorisation chol_mfma_kernel<NB <= 9>
+// and its A/B variants (see ewarp_dev.h, ewh_set_kernel_mode).
+#include "ewarp_dev.h"
+
+namespace ewh_dev {
+namespace {
+
+template <int NB, int FULL = 0, int W = default_waves(NB), int ALG = 0>
+void launch_chol_mfma(const CholJob* jobs, int B, long long u0, long long n, int b_off, const double* theta, int ldth,
+                      double* units, hipStream_t st) {
+  hipLaunchKernelGGL(HIP_KERNEL_NAME(chol_mfma_kernel<NB, FULL, W, ALG, 0>), dim3((unsigned)n), dim3(64), 0, st, jobs,
+                     B, u0, b_off, theta, ldth, units, nullptr, 0, 0);
+}
+
+}  // namespace
+
+int launch_chol_small(int mode, int nb, const CholJob* jobs, int B, long long u0, long long n, int b_off,
+                      const double* theta, int ldth, double* units, hipStream_t st) {
+  // A/B variants (NB = 8, the C3 reduced width)
+  if (nb == 8 && mode >= 3) {
+    switch (mode) {
+      case 3: launch_chol_mfma<8, 1, 1, 1>(jobs, B, u0, n, b_off, theta, ldth, units, st); return 0;  // 1 wave/SIMD
+      case 4: launch_chol_mfma<8, 0, 2, 1>(jobs, B, u0, n, b_off, theta, ldth, units, st); return 0;  // LDL, looped
+      case 5: launch_chol_mfma<8, 1, 2, 0>(jobs, B, u0, n, b_off, theta, ldth, units, st); return 0;  // Cholesky, unrolled
+      case 6: launch_chol_mfma<8, 0, 2, 2>(jobs, B, u0, n, b_off, theta, ldth, units, st); return 0;  // LDL, LDS bcast
+      default: break;
+    }
+  }
+  if (mode == 1) return 1;
+  // default: LDL^T panel, panel steps unrolled up to NB = 8; mode 2: the
+  // round-1 Cholesky panel (looped) as the A/B baseline
+  const bool base = mode == 2;
+#define EWH_CHOL_CASE(NBV)                                                                                   \
+  case NBV:                                                                                                  \
+    if (base) launch_chol_mfma<NBV, 0, default_waves(NBV), 0>(jobs, B, u0, n, b_off, theta, ldth, units, st); \
+    else launch_chol_mfma<NBV, (NBV <= 8), default_waves(NBV), 1>(jobs, B, u0, n, b_off, theta, ldth, units, st); \
+    return 0;
+  switch (nb) {
+    EWH_CHOL_CASE(1)
+    EWH_CHOL_CASE(2)
+    EWH_CHOL_CASE(3)
+    EWH_CHOL_CASE(4)
+    EWH_CHOL_CASE(5)
+    EWH_CHOL_CASE(6)
+    EWH_CHOL_CASE(7)
+    EWH_CHOL_CASE(8)
+    EWH_CHOL_CASE(9)
+    default: return 1;
+  }
+#undef EWH_CHOL_CASE
+}
+
+}  // namespace ewh_dev

@@ -1,0 +1,83 @@
+// contract.hip — instantiations of the contraction kernels (see ewarp_dev.h).
+#include "ewarp_dev.h"
+
+namespace ewh_dev {
+namespace {
+
+template <int NB>
+void launch_contract(const PsrDev& P, const double* w, const double* beta, const double* s, const double* fac,
+                     double* G, int nb_samples, hipStream_t st) {
+  const size_t lds = (size_t)(CT_ROWS * 16 * NB + CT_ROWS) * sizeof(double);
+  hipLaunchKernelGGL(HIP_KERNEL_NAME(contract_mfma_kernel<NB>), dim3(nb_samples), dim3(256), lds, st, P, w, beta, s,
+                     fac, G);
+}
+
+int dispatch_contract(int nb, const PsrDev& P, const double* w, const double* beta, const double* s,
+                      const double* fac, double* G, int nb_samples, hipStream_t st) {
+  switch (nb) {
+    case 1: launch_contract<1>(P, w, beta, s, fac, G, nb_samples, st); break;
+    case 2: launch_contract<2>(P, w, beta, s, fac, G, nb_samples, st); break;
+    case 3: launch_contract<3>(P, w, beta, s, fac, G, nb_samples, st); break;
+    case 4: launch_contract<4>(P, w, beta, s, fac, G, nb_samples, st); break;
+    case 5: launch_contract<5>(P, w, beta, s, fac, G, nb_samples, st); break;
+    case 6: launch_contract<6>(P, w, beta, s, fac, G, nb_samples, st); break;
+    case 7: launch_contract<7>(P, w, beta, s, fac, G, nb_samples, st); break;
+    case 8: launch_contract<8>(P, w, beta, s, fac, G, nb_samples, st); break;
+    case 9: launch_contract<9>(P, w, beta, s, fac, G, nb_samples, st); break;
+    case 10: launch_contract<10>(P, w, beta, s, fac, G, nb_samples, st); break;
+    case 11: launch_contract<11>(P, w, beta, s, fac, G, nb_samples, st); break;
+    case 12: launch_contract<12>(P, w, beta, s, fac, G, nb_samples, st); break;
+    case 13: launch_contract<13>(P, w, beta, s, fac, G, nb_samples, st); break;
+    default: return set_err(EWH_E_UNSUPPORTED, "basis too wide for the contraction kernel (> 207 columns)");
+  }
+  return 0;
+}
+
+template <int NB>
+int launch_contract2(const PsrDev& P, const double* w, const double* beta, double* s, long long s_stride, double* G,
+                     int nb_samples, hipStream_t st) {
+  const size_t lds = (size_t)(2 * CT_ROWS * 16 * NB + 3 * CT_ROWS) * sizeof(double);
+  static bool attr = false;
+  if (!attr) {
+    EWH_HIP(hipFuncSetAttribute((const void*)contract2_kernel<NB>, hipFuncAttributeMaxDynamicSharedMemorySize,
+                                (int)lds));
+    attr = true;
+  }
+  hipLaunchKernelGGL(HIP_KERNEL_NAME(contract2_kernel<NB>), dim3(nb_samples), dim3(256), lds, st, P, w, beta, s,
+                     s_stride, G);
+  return 0;
+}
+
+int dispatch_contract2(int nb, const PsrDev& P, const double* w, const double* beta, double* s, long long s_stride,
+                       double* G, int nb_samples, hipStream_t st) {
+  switch (nb) {
+    case 1: return launch_contract2<1>(P, w, beta, s, s_stride, G, nb_samples, st);
+    case 2: return launch_contract2<2>(P, w, beta, s, s_stride, G, nb_samples, st);
+    case 3: return launch_contract2<3>(P, w, beta, s, s_stride, G, nb_samples, st);
+    case 4: return launch_contract2<4>(P, w, beta, s, s_stride, G, nb_samples, st);
+    case 5: return launch_contract2<5>(P, w, beta, s, s_stride, G, nb_samples, st);
+    case 6: return launch_contract2<6>(P, w, beta, s, s_stride, G, nb_samples, st);
+    case 7: return launch_contract2<7>(P, w, beta, s, s_stride, G, nb_samples, st);
+    case 8: return launch_contract2<8>(P, w, beta, s, s_stride, G, nb_samples, st);
+    case 9: return launch_contract2<9>(P, w, beta, s, s_stride, G, nb_samples, st);
+    case 10: return launch_contract2<10>(P, w, beta, s, s_stride, G, nb_samples, st);
+    case 11: return launch_contract2<11>(P, w, beta, s, s_stride, G, nb_samples, st);
+    case 12: return launch_contract2<12>(P, w, beta, s, s_stride, G, nb_samples, st);
+    case 13: return launch_contract2<13>(P, w, beta, s, s_stride, G, nb_samples, st);
+    default: return set_err(EWH_E_UNSUPPORTED, "basis too wide for the contraction kernel (> 207 columns)");
+  }
+}
+
+}  // namespace
+
+int launch_contract_nb(int nb, const PsrDev& P, const double* w, const double* beta, const double* s,
+                       const double* fac, double* G, int nb_samples, hipStream_t st) {
+  return dispatch_contract(nb, P, w, beta, s, fac, G, nb_samples, st);
+}
+
+int launch_contract2_nb(int nb, const PsrDev& P, const double* w, const double* beta, double* s,
+                        long long s_stride, double* G, int nb_samples, hipStream_t st) {
+  return dispatch_contract2(nb, P, w, beta, s, s_stride, G, nb_samples, st);
+}
+
+}  // namespace ewh_dev

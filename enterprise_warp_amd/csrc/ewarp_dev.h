@@ -1,0 +1,940 @@
+// ewarp_dev.h — device-side types, helpers and kernel templates shared by the
+// translation units of libewarp_hip.so (split so hipcc builds them in parallel):
+//   ewarp_hip.hip     host side (C ABI), non-template kernels
+//   chol_small.hip    chol_mfma_kernel<NB <= 9> (register-resident factorisation)
+//   chol_partial.hip  chol_mfma_kernel<..., KEEP> (correlated common process)
+//   chol_big.hip      chol_big_kernel<NB 10..16>
+//   contract.hip      contract_mfma_kernel / contract2_kernel
+// See ewarp_hip.hip for the formulation.
+#pragma once
+#include <hip/hip_runtime.h>
+
+#include <algorithm>
+#include <cmath>
+#include <cstdint>
+#include <cstring>
+#include <string>
+#include <type_traits>
+#include <vector>
+
+#include "ewarp_hip.h"
+
+namespace ewh_dev {
+
+// thread-local error message of the C ABI (defined in ewarp_hip.hip)
+int set_err(int code, const std::string& msg);
+
+#define EWH_HIP(expr)                                                          \
+  do {                                                                         \
+    hipError_t e_ = (expr);                                                    \
+    if (e_ != hipSuccess)                                                      \
+      return ::ewh_dev::set_err(EWH_E_HIP, std::string(#expr) + ": " + hipGetErrorString(e_)); \
+  } while (0)
+
+constexpr int MFMA_NB_MAX = 9;
+constexpr int CONTRACT2_NB_MAX = 13;
+constexpr int default_waves(int nb) { return nb <= 8 ? 2 : 1; }
+
+typedef double v4d __attribute__((ext_vector_type(4)));
+
+// ----------------------------------------------------------------------------
+// device helpers
+// ----------------------------------------------------------------------------
+__device__ __forceinline__ double pref_val(const ewh_pref& r, const double* th) {
+  return r.idx >= 0 ? th[r.idx] : r.cval;
+}
+
+// Device form of one spectral entry (built from ewh_spec_entry at create).
+// phi is evaluated as one exp of a sum of logs:
+//   POWERLAW  A^2/(12 pi^2) fyr^(g-3) f^-g df = exp(a + 2 ln10 lgA + (g-3) ln fyr - g ln f)
+//   TURNOVER  A^2/(12 pi^2) fyr^-3 ((f+fc)/fyr)^-g df
+//             = exp(a + 2 ln10 lgA - 3 ln fyr - g (ln(f+fc) - ln fyr)),  fc = 10^fc if fc < 0
+//   FREESPEC  10^(2 rho) = exp(2 ln10 rho)
+//   CONST     v0
+// with a = ln(df / (12 pi^2)); the same quantities as [ent] utils.powerlaw,
+// the reference's powerlaw_bpl (enterprise_models.py:553-563) and
+// [ent] gp_priors.free_spectrum, re-associated (relative error ~1e-14).
+struct DSpec {
+  int kind, col;
+  int i0, i1, i2, pad_;
+  double v0, v1, v2;     // constant values of the three parameters
+  double a, lnf, lnfyr, f;
+};
+
+__device__ __forceinline__ double dpar(int idx, double cval, const double* th) {
+  return idx >= 0 ? th[idx] : cval;
+}
+
+constexpr double LN10 = 2.302585092994045684;
+
+// spec_phi_body: the arithmetic; spec_phi: an out-of-line copy for the schur and
+// LDS-Cholesky kernels (ROCm 7.2 clang crashes in the CGSCC inliner when one
+// inlined copy serves both); the register-resident kernels inline the body
+// (a call there reserves a scratch frame the unrolled factorisation then
+// spills into).
+template <int DUMMY = 0>
+__device__ __forceinline__ double spec_phi_body(const DSpec& s, const double* th) {
+  switch (s.kind) {
+    case EWH_SPEC_POWERLAW: {
+      const double lgA = dpar(s.i0, s.v0, th), gam = dpar(s.i1, s.v1, th);
+      return exp(s.a + 2.0 * LN10 * lgA + (gam - 3.0) * s.lnfyr - gam * s.lnf);
+    }
+    case EWH_SPEC_TURNOVER: {
+      const double lgA = dpar(s.i0, s.v0, th), gam = dpar(s.i1, s.v1, th);
+      double fc = dpar(s.i2, s.v2, th);
+      if (fc < 0) fc = exp(LN10 * fc);
+      return exp(s.a + 2.0 * LN10 * lgA - 3.0 * s.lnfyr - gam * (log(s.f + fc) - s.lnfyr));
+    }
+    case EWH_SPEC_FREESPEC:
+      return exp(2.0 * LN10 * dpar(s.i0, s.v0, th));
+    case EWH_SPEC_CONST:
+      return s.v0;
+    default:
+      return __builtin_nan("");
+  }
+}
+
+static __device__ __noinline__ double spec_phi(const DSpec& s, const double* th) { return spec_phi_body(s, th); }
+
+// running log-determinant without a log per term: product of frexp mantissas
+// (each in [0.5, 1): >= 2^-1000 after 1000 terms, no underflow) + exponent sum.
+struct LogAcc {
+  double mant = 1.0;
+  int ex = 0;
+  __device__ __forceinline__ void add(double x) {
+    mant *= __builtin_amdgcn_frexp_mant(x);   // <= 1000 terms: no renormalisation needed
+    ex += __builtin_amdgcn_frexp_exp(x);
+  }
+  __device__ __forceinline__ double value() const { return log(mant) + ex * 0.69314718055994530942; }
+};
+
+__device__ __forceinline__ double readlane_d(double x, int lane) {
+  const int lo = __builtin_amdgcn_readlane(__double2loint(x), lane);
+  const int hi = __builtin_amdgcn_readlane(__double2hiint(x), lane);
+  return __hiloint2double(hi, lo);
+}
+
+// 1/sqrt(a): hardware estimate + two Newton steps (~1 ulp).
+__device__ __forceinline__ double rsqrt_nr(double a) {
+  double y = __builtin_amdgcn_rsq(a);
+  const double h = 0.5 * a;
+  double t = fma(-h * y, y, 0.5);
+  y = fma(y, t, y);
+  t = fma(-h * y, y, 0.5);
+  return fma(y, t, y);
+}
+
+// XCD-aware unit order: the dispatcher deals workgroup b to XCD b % 8, so
+// XCD x gets the contiguous unit range [x q, (x+1) q) (q = n / 8; the n % 8
+// tail maps to itself).  Units are pulsar-major, so each pulsar's reduced
+// matrix is fetched into ~one XCD's L2 instead of all eight.
+__device__ __forceinline__ long long xcd_unit(unsigned b, unsigned n) {
+  const unsigned q = n >> 3;
+  return b < (q << 3) ? (long long)(b & 7) * q + (b >> 3) : (long long)b;
+}
+
+// 1/a: hardware estimate + two Newton steps (~1 ulp).
+__device__ __forceinline__ double rcp_nr(double a) {
+  double y = __builtin_amdgcn_rcp(a);
+  double e = fma(-a, y, 1.0);
+  y = fma(y, e, y);
+  e = fma(-a, y, 1.0);
+  return fma(y, e, y);
+}
+
+__device__ __forceinline__ double wave_sum(double v) {
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o);
+  return v;
+}
+
+// 256-thread block sum; `scratch` holds >= 4 doubles.
+static __device__ double block_sum256(double v, double* scratch) {
+  v = wave_sum(v);
+  const int w = threadIdx.x >> 6;
+  __syncthreads();
+  if ((threadIdx.x & 63) == 0) scratch[w] = v;
+  __syncthreads();
+  double t = scratch[0] + scratch[1] + scratch[2] + scratch[3];
+  __syncthreads();
+  return t;
+}
+
+// ----------------------------------------------------------------------------
+// per-pulsar device tables
+// ----------------------------------------------------------------------------
+constexpr int CT_ROWS = 32;   // TOA rows per contraction tile (8 MFMA k-steps); T_aug is padded by this many zero rows
+
+struct PsrDev {
+  int n_toa, m, ld, nb;      // varying layout: T_aug is n_toa x ld, r at ld-1
+  int n_epoch;
+  const double* T;           // n_toa x ld row-major
+  const double* sig2;        // toaerr^2
+  const int* efac_slot;
+  const int* equad_slot;
+  const ewh_pref* slots;
+  const int* ep_start;
+  const int* ep_stop;
+  const int* ep_slot;
+  int n_bgroup;              // theta-dependent chromatic basis groups (0: none)
+  const int* col_bgroup;     // ld entries, -1 = fixed column
+  const double* ln_chrom;    // n_toa: ln(1400 / nu)
+  const ewh_pref* bgroup;    // n_bgroup: chromatic index per group
+  const int* toa_ep;         // n_toa + CT_ROWS: 2 e + (last TOA of e), -1 = no epoch (pad rows -1)
+};
+
+// One factorisation job: (pulsar, sample) -> matrix + diagonal update.
+struct CholJob {
+  const double* mats;        // matrix of sample b at mats + (b - b_off) * mstride
+  long long mstride;         // 0: one matrix shared by every sample
+  int ld;                    // leading dimension (= 16 * NB)
+  int mreal;                 // columns with a phi entry (0..mreal-1); r at ld-1
+  const int* col_ptr;        // CSR of spectral entries over mreal columns
+  const DSpec* spec;
+  const double* K;           // additive constant, K[(b - b_off) * kstride]
+  int kstride;
+  int fail;                  // 1: lead block not positive definite -> -inf
+};
+
+// ----------------------------------------------------------------------------
+// fp64 MFMA contraction G = T_aug^T W T_aug - sum_e beta_e s_e s_e^T
+// One 256-thread workgroup (4 waves) per sample; the NB(NB+1)/2 upper 16x16
+// output blocks are dealt round-robin to the waves; 32-row TOA tiles are
+// staged in LDS and shared by the four waves.
+// ----------------------------------------------------------------------------
+template <int NB>
+__global__ __launch_bounds__(256) void contract_mfma_kernel(PsrDev P, const double* __restrict__ w,
+                                                            const double* __restrict__ beta,
+                                                            const double* __restrict__ s,
+                                                            const double* __restrict__ fac,
+                                                            double* __restrict__ G) {
+  constexpr int LD = 16 * NB;
+  constexpr int NBLK = NB * (NB + 1) / 2;
+  constexpr int SLOTS = (NBLK + 3) / 4;
+  extern __shared__ __attribute__((aligned(16))) double smem[];
+  double* tile = smem;                     // CT_ROWS x LD
+  double* wt = smem + CT_ROWS * LD;        // CT_ROWS weights
+  const int bl = blockIdx.x;
+  const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63, q = lane >> 4, c = lane & 15;
+
+  int bi[SLOTS], bj[SLOTS];
+  bool valid[SLOTS];
+#pragma unroll
+  for (int sl = 0; sl < SLOTS; ++sl) {
+    int blk = wave + 4 * sl;
+    valid[sl] = blk < NBLK;
+    int i = 0;
+    while (blk >= NB - i && i < NB - 1) { blk -= NB - i; ++i; }
+    bi[sl] = i;
+    bj[sl] = i + blk;
+  }
+  v4d acc[SLOTS];
+#pragma unroll
+  for (int sl = 0; sl < SLOTS; ++sl) acc[sl] = v4d{0.0, 0.0, 0.0, 0.0};
+
+  // pass 0: TOA rows (weights w), pass 1: epoch rows (weights -beta)
+  for (int pass = 0; pass < 2; ++pass) {
+    const int nrows = pass == 0 ? P.n_toa : P.n_epoch;
+    const double* src = pass == 0 ? P.T : s + (long long)bl * P.n_epoch * LD;
+    const double* wsrc = pass == 0 ? w + (long long)bl * P.n_toa : beta + (long long)bl * P.n_epoch;
+    const double wsign = pass == 0 ? 1.0 : -1.0;
+    for (int t0 = 0; t0 < nrows; t0 += CT_ROWS) {
+      const int rows = min(CT_ROWS, nrows - t0);
+      if (pass == 0 && P.n_bgroup) {   // theta-dependent chromatic columns: scale per TOA
+        for (int idx = threadIdx.x; idx < CT_ROWS * LD; idx += 256) {
+          const int r = idx / LD, cc = idx - r * LD;
+          double v = idx < rows * LD ? src[(long long)t0 * LD + idx] : 0.0;
+          const int g = P.col_bgroup[cc];
+          if (g >= 0 && r < rows) v *= fac[((long long)bl * P.n_bgroup + g) * P.n_toa + t0 + r];
+          tile[idx] = v;
+        }
+      } else {
+        for (int idx = threadIdx.x; idx < CT_ROWS * LD; idx += 256)
+          tile[idx] = idx < rows * LD ? src[(long long)t0 * LD + idx] : 0.0;
+      }
+      if (threadIdx.x < CT_ROWS) wt[threadIdx.x] = threadIdx.x < rows ? wsign * wsrc[t0 + threadIdx.x] : 0.0;
+      __syncthreads();
+#pragma unroll
+      for (int kk = 0; kk < CT_ROWS / 4; ++kk) {
+        const int row = 4 * kk + q;
+        const double wr = wt[row];
+        const double* trow = tile + row * LD + c;
+#pragma unroll
+        for (int sl = 0; sl < SLOTS; ++sl) {
+          if (valid[sl]) {
+            const double a = wr * trow[16 * bi[sl]];
+            const double b = trow[16 * bj[sl]];
+            acc[sl] = __builtin_amdgcn_mfma_f64_16x16x4f64(a, b, acc[sl], 0, 0, 0);
+          }
+        }
+      }
+      __syncthreads();
+    }
+  }
+  // epilogue: C/D layout lane -> (row q + 4r, col c); mirror to the lower half,
+  // unit diagonal on pad columns (m .. LD-2) so they factor as identity.
+  double* out = G + (long long)bl * LD * LD;
+#pragma unroll
+  for (int sl = 0; sl < SLOTS; ++sl) {
+    if (!valid[sl]) continue;
+#pragma unroll
+    for (int r = 0; r < 4; ++r) {
+      const int row = 16 * bi[sl] + q + 4 * r, col = 16 * bj[sl] + c;
+      double v = acc[sl][r];
+      if (row == col && row >= P.m && row < LD - 1) v = 1.0;
+      out[(long long)row * LD + col] = v;
+      out[(long long)col * LD + row] = v;
+    }
+  }
+}
+
+// ----------------------------------------------------------------------------
+// fp64 MFMA contraction, pipelined (default for pulsars without theta-dependent
+// basis columns).  One 256-thread workgroup (4 waves) per sample:
+//   G = T_aug^T W T_aug - sum_e beta_e s_e s_e^T,  s_e = sum_{t in e} w_t T_aug[t].
+//  * TOA tiles of CT_ROWS rows are copied global -> LDS by global_load_lds
+//    (16 B per lane, 1 KiB per wave-instruction; T_aug is contiguous and padded
+//    by CT_ROWS zero rows) into two buffers: tile i+1 streams in while the
+//    MFMAs run on tile i.
+//  * Wave WAVE owns the upper blocks blk = WAVE + 4 sl (compile-time, so the
+//    operand set is known): per k-step it reads T[row][16 j + c] once per block
+//    column j it touches and forms w_row * T[row][16 i + c] once per block row i.
+//  * ECORR: the epoch sums s_e are accumulated from the same LDS tile (thread
+//    = column; epochs are contiguous TOA runs that may straddle tiles) and
+//    written to a per-sample scratch; a second pass runs them through the same
+//    MFMA loop with weights -beta_e.  No second read of T from HBM.
+// ----------------------------------------------------------------------------
+typedef __attribute__((address_space(3))) void lds_void_t;
+typedef __attribute__((address_space(1))) void gbl_void_t;
+
+// block index blk of the upper triangle (row-major over i <= j) -> (i, j)
+constexpr int tri_i(int nb, int blk) {
+  int i = 0;
+  while (blk >= nb - i) { blk -= nb - i; ++i; }
+  return i;
+}
+constexpr int tri_j(int nb, int blk) {
+  int i = 0;
+  while (blk >= nb - i) { blk -= nb - i; ++i; }
+  return i + blk;
+}
+// does wave `wave` (blocks wave + 4 sl) touch block column j as a row (A) / at all?
+constexpr bool wave_uses_row(int nb, int wave, int j) {
+  for (int blk = wave; blk < nb * (nb + 1) / 2; blk += 4)
+    if (tri_i(nb, blk) == j) return true;
+  return false;
+}
+constexpr bool wave_uses(int nb, int wave, int j) {
+  for (int blk = wave; blk < nb * (nb + 1) / 2; blk += 4)
+    if (tri_i(nb, blk) == j || tri_j(nb, blk) == j) return true;
+  return false;
+}
+
+template <int NB, int WAVE>
+__device__ __forceinline__ void contract2_body(const PsrDev& P, const double* __restrict__ wrow,
+                                               const double* __restrict__ brow, double* __restrict__ srow,
+                                               double* __restrict__ Gout) {
+  extern __shared__ __attribute__((aligned(16))) double smem[];
+  constexpr int LD = 16 * NB;
+  constexpr int NBLK = NB * (NB + 1) / 2;
+  constexpr int SLOTS = (NBLK - WAVE + 3) / 4;
+  constexpr int TILE = CT_ROWS * LD;                 // doubles per tile
+  constexpr int CHUNKS = TILE * 8 / 1024 / 4;        // 1-KiB glds pieces per wave per tile (= NB)
+  static_assert(CHUNKS * 4 * 1024 == TILE * 8, "tile must split into 4 x NB pieces of 1 KiB");
+  // LDS: [2][TILE] tiles | [2][CT_ROWS] weights | [2][CT_ROWS] int epoch flags
+  const int tid = threadIdx.x, lane = tid & 63, q = lane >> 4, c = lane & 15;
+  double* const wbase = smem + 2 * TILE;
+  int* const ebase = (int*)(smem + 2 * TILE + 2 * CT_ROWS);
+
+  v4d acc[SLOTS > 0 ? SLOTS : 1];
+#pragma unroll
+  for (int sl = 0; sl < SLOTS; ++sl) acc[sl] = v4d{0.0, 0.0, 0.0, 0.0};
+
+  const bool ecorr = P.n_epoch > 0;
+  double eacc = 0.0;                                 // running s_e of column `tid`
+  // pass 0: TOA rows (weights w); pass 1: epoch rows (weights -beta)
+  for (int pass = 0; pass < (ecorr ? 2 : 1); ++pass) {
+    const int nrows = pass == 0 ? P.n_toa : P.n_epoch;
+    const double* src = pass == 0 ? P.T : srow;
+    const double* wsrc = pass == 0 ? wrow : brow;
+    const double wsign = pass == 0 ? 1.0 : -1.0;
+    const int ntile = (nrows + CT_ROWS - 1) / CT_ROWS;
+    auto issue = [&](int it) {
+      const char* g = (const char*)(src + (long long)it * TILE) + (WAVE * CHUNKS) * 1024 + lane * 16;
+      char* l = (char*)(smem + (it & 1) * TILE) + (WAVE * CHUNKS) * 1024;
+#pragma unroll
+      for (int k = 0; k < CHUNKS; ++k)
+        __builtin_amdgcn_global_load_lds((gbl_void_t*)(g + k * 1024), (lds_void_t*)(l + k * 1024), 16, 0, 0);
+    };
+    double wv = 0.0;
+    int ev = -1;
+    auto small = [&](int it) {
+      const int t = it * CT_ROWS + tid;
+      wv = (tid < CT_ROWS && t < nrows) ? wsign * wsrc[t] : 0.0;
+      ev = (pass == 0 && tid < CT_ROWS) ? P.toa_ep[t] : -1;
+    };
+    issue(0);
+    small(0);
+    if (tid < CT_ROWS) {
+      wbase[tid] = wv;
+      ebase[tid] = ev;
+    }
+    __syncthreads();
+    for (int it = 0; it < ntile; ++it) {
+      const int cur = it & 1;
+      if (it + 1 < ntile) {
+        issue(it + 1);
+        small(it + 1);
+      }
+      const double* tile = smem + cur * TILE;
+      const double* wt = wbase + cur * CT_ROWS;
+#pragma unroll
+      for (int kk = 0; kk < CT_ROWS / 4; ++kk) {
+        const int row = 4 * kk + q;
+        const double wr = wt[row];
+        const double* trow = tile + row * LD + c;
+        double tv[NB], av[NB];
+        static_for<0, NB>([&](auto J) {
+          constexpr int j = decltype(J)::value;
+          if constexpr (wave_uses(NB, WAVE, j)) tv[j] = trow[16 * j];
+          if constexpr (wave_uses_row(NB, WAVE, j)) av[j] = wr * tv[j];
+        });
+        static_for<0, SLOTS>([&](auto SL) {
+          constexpr int blk = WAVE + 4 * decltype(SL)::value;
+          constexpr int bi = tri_i(NB, blk), bj = tri_j(NB, blk);
+          acc[decltype(SL)::value] = __builtin_amdgcn_mfma_f64_16x16x4f64(av[bi], tv[bj], acc[decltype(SL)::value], 0, 0, 0);
+        });
+      }
+      if (pass == 0 && ecorr && tid < LD) {          // epoch sums of column tid
+        const double* tcol = tile + tid;
+        const int* ecur = ebase + cur * CT_ROWS;
+        for (int r = 0; r < CT_ROWS; ++r) {
+          const int e = ecur[r];
+          if (e >= 0) {
+            eacc = fma(wt[r], tcol[r * LD], eacc);
+            if (e & 1) {
+              srow[(long long)(e >> 1) * LD + tid] = eacc;
+              eacc = 0.0;
+            }
+          }
+        }
+      }
+      if (it + 1 < ntile && tid < CT_ROWS) {
+        wbase[(cur ^ 1) * CT_ROWS + tid] = wv;
+        ebase[(cur ^ 1) * CT_ROWS + tid] = ev;
+      }
+      __syncthreads();                               // drains the glds of tile it+1 (vmcnt(0))
+    }
+    if (pass == 0 && ecorr) __threadfence_block();   // s_e rows visible to the epoch pass
+    __syncthreads();
+  }
+  // epilogue: C/D layout lane -> (row q + 4r, col c); mirror to the lower half,
+  // unit diagonal on pad columns (m .. LD-2) so they factor as identity.
+  static_for<0, SLOTS>([&](auto SL) {
+    constexpr int blk = WAVE + 4 * decltype(SL)::value;
+    constexpr int bi = tri_i(NB, blk), bj = tri_j(NB, blk);
+#pragma unroll
+    for (int r = 0; r < 4; ++r) {
+      const int row = 16 * bi + q + 4 * r, col = 16 * bj + c;
+      double v = acc[decltype(SL)::value][r];
+      if (row == col && row >= P.m && row < LD - 1) v = 1.0;
+      Gout[(long long)row * LD + col] = v;
+      Gout[(long long)col * LD + row] = v;
+    }
+  });
+}
+
+template <int NB>
+__global__ __launch_bounds__(256) void contract2_kernel(PsrDev P, const double* __restrict__ w,
+                                                        const double* __restrict__ beta, double* __restrict__ s,
+                                                        long long s_stride, double* __restrict__ G) {
+  constexpr int LD = 16 * NB;
+  const int bl = blockIdx.x;
+  const double* wrow = w + (long long)bl * P.n_toa;
+  const double* brow = beta + (long long)bl * P.n_epoch;
+  double* srow = s + (long long)bl * s_stride;
+  double* Gout = G + (long long)bl * LD * LD;
+  switch (threadIdx.x >> 6) {
+    case 0: contract2_body<NB, 0>(P, wrow, brow, srow, Gout); break;
+    case 1: contract2_body<NB, 1>(P, wrow, brow, srow, Gout); break;
+    case 2: contract2_body<NB, 2>(P, wrow, brow, srow, Gout); break;
+    default: contract2_body<NB, 3>(P, wrow, brow, srow, Gout); break;
+  }
+}
+
+// ----------------------------------------------------------------------------
+// batched Cholesky, MFMA register-blocked: one wave (64 lanes) per unit.
+// The upper triangle of the LD x LD matrix (LD = 16 NB) is held as 16x16
+// blocks in the v_mfma_f64_16x16x4_f64 C/D layout (lane l, reg r <-> row
+// (l>>4) + 4r, col l&15).  Factor A = U^T U (upper, as LAPACK dpotrf 'U'
+// behind scipy cho_factor).  Per block row bb the 16 pivots of the panel are
+// done by VALU (pivot by readlane, 1/sqrt by v_rsq_f64 + Newton, row k
+// broadcast by ds_bpermute, only the rows that can still change are
+// touched); trailing blocks get A_ij -= U_bi^T U_bj by four MFMAs each with
+// no data movement — register s of a C/D-layout block IS the MFMA A / B
+// operand of k-slice s.
+//
+// Three phases keep at most 26 blocks live for NB = 8 (36 in a plain
+// right-looking order): (1) factor block rows 0..H-1 (H = NB/2) with the
+// trailing update restricted to those rows; (2) load the trailing A22
+// triangle and apply the H panel rows to it; (3) factor A22.  Same
+// arithmetic, re-ordered (left-looking at the 2x2 block level).
+// ----------------------------------------------------------------------------
+template <int NB>
+struct Split {
+  // block rows of phase 1: NB/2, except 3 of 8 (phase 1's 21 blocks + panel
+  // temporaries then fit 256 VGPRs without spills; phase 2 runs row by row)
+  static constexpr int H = NB == 8 ? 3 : NB / 2;
+  static constexpr int M = NB - H;                    // A22 block order
+  static constexpr int n1 = H * NB - H * (H - 1) / 2; // blocks (i < H, j >= i)
+  static constexpr int n2 = M * (M + 1) / 2;          // blocks (H <= i <= j)
+  static constexpr int i1(int i, int j) { return i * NB - (i * (i - 1)) / 2 + (j - i); }
+  static constexpr int i2(int i, int j) { return (i - H) * M - ((i - H) * (i - H - 1)) / 2 + (j - i); }
+};
+
+// compile-time loop: f(std::integral_constant<int, I>) for I in [B, E)
+template <int B, int E, typename F>
+__device__ __forceinline__ void static_for(F&& f) {
+  if constexpr (B < E) {
+    f(std::integral_constant<int, B>{});
+    static_for<B + 1, E>(f);
+  }
+}
+
+// A -= U_i^T U_j : four f64 MFMAs (A operand = -U_i)
+__device__ __forceinline__ void syrk_update(v4d& C, const v4d& Ui, const v4d& Uj) {
+#pragma unroll
+  for (int sk = 0; sk < 4; ++sk) C = __builtin_amdgcn_mfma_f64_16x16x4f64(-Ui[sk], Uj[sk], C, 0, 0, 0);
+}
+
+// FULL: 1 = every panel step unrolled (large code), 0 = runtime loop over the
+// row's lane group (the default)
+// W: waves per SIMD the register budget is cut for (2 -> 256 VGPRs: the NB = 8
+// three-phase kernel fits with no spills, so two units share each SIMD and one's
+// MFMAs overlap the other's VALU / LDS latency).
+// ALG: panel form.  0 = Cholesky panel (row k scaled by 1/sqrt(pivot) before it
+// is broadcast); 1 = square-root-free LDL^T panel: row k is broadcast raw while
+// 1/d_k is formed, the lane's rows take the update with u_i = A_ki / d_k, and
+// the 16 rows of the block row are scaled to U = D^-1/2 V together at the end
+// (one vector rsqrt per register instead of one serial rsqrt per pivot).  The
+// per-pivot dependency chain drops the scale -> ds_bpermute leg; log|Sigma| =
+// sum log d_k is accumulated per block row from the lanes' own pivots.
+// LDL^T panel of block row BB over the blocks blk(j), j = BB..NB-1 (C/D
+// layout, upper triangle), used by the register-resident kernels: the 16
+// pivots are factored by VALU (ALG 1: row k broadcast by ds_bpermute, ALG 2:
+// through the per-wave LDS `rowbuf`), then the block row is scaled to
+// U = D^-1/2 V.  Accumulates log d_k (one lane per row) and d_k > 0 per lane.
+template <int NB, int FULL, int ALG, typename BBt, typename Blk>
+__device__ __forceinline__ void panel_ldl_row(BBt BBc, Blk&& blk, int q, int c, LogAcc& ldet, bool& ok,
+                                              double* rowbuf) {
+  constexpr int LD = 16 * NB;
+  (void)rowbuf;
+  (void)LD;
+  constexpr int bb = decltype(BBc)::value;
+  static_for<0, 4>([&](auto KR) {
+    constexpr int kr = decltype(KR)::value;
+    auto step = [&](const int kq) {
+      const int k = 4 * kr + kq;
+      const double d = readlane_d(blk(BBc)[kr], 16 * kq + k);            // wave-uniform pivot
+      // raw row k: A[k][q + 4r] for this lane's rows (masked to rows > k) and
+      // A[k][col c] of every block of the row; both in flight while 1/d forms
+      double ui[4];
+      double rk[NB];
+      if constexpr (ALG == 2) {
+        // LDS broadcast: the 16 lanes of quad kq store row k of every block
+        // (one ds_write_b64 per block), every lane reads it back with 16
+        // distinct addresses per read (broadcast, bank-conflict free) --
+        // several times cheaper on the CU's LDS than two ds_bpermute_b32
+        // per double.  One wave per workgroup and LDS ops of a wave run in
+        // order, so no barrier: the asm fences only stop the compiler from
+        // moving the reads above the other lanes' writes.
+        double* rb = rowbuf + (k & 1) * LD;
+        if (q == kq) {
+          static_for<bb, NB>([&](auto JJ) {
+            constexpr int j = decltype(JJ)::value;
+            rb[16 * j + c] = blk(JJ)[kr];
+          });
+        }
+        asm volatile("" ::: "memory");
+        static_for<kr, 4>([&](auto R) {
+          constexpr int r = decltype(R)::value;
+          const double v = rb[16 * bb + q + 4 * r];
+          ui[r] = (r > kr || q > kq) ? v : 0.0;
+        });
+        static_for<bb, NB>([&](auto JJ) {
+          constexpr int j = decltype(JJ)::value;
+          rk[j] = rb[16 * j + c];
+        });
+        asm volatile("" ::: "memory");
+      } else {
+        static_for<kr, 4>([&](auto R) {
+          constexpr int r = decltype(R)::value;
+          const double v = __shfl(blk(BBc)[kr], 16 * kq + q + 4 * r);
+          ui[r] = (r > kr || q > kq) ? v : 0.0;
+        });
+        static_for<bb, NB>([&](auto JJ) {
+          constexpr int j = decltype(JJ)::value;
+          rk[j] = __shfl(blk(JJ)[kr], 16 * kq + c);
+        });
+      }
+      const double dinv = rcp_nr(d);
+      static_for<kr, 4>([&](auto R) { ui[decltype(R)::value] *= dinv; });
+      static_for<bb, NB>([&](auto JJ) {
+        constexpr int j = decltype(JJ)::value;
+        static_for<kr, 4>([&](auto R) {
+          constexpr int r = decltype(R)::value;
+          blk(JJ)[r] = fma(-ui[r], rk[j], blk(JJ)[r]);
+        });
+      });
+    };
+    constexpr int nk = (bb == NB - 1 && kr == 3) ? 3 : 4;   // the r column is not pivoted
+    if constexpr (FULL) {
+      static_for<0, nk>([&](auto KQ) {
+        step(decltype(KQ)::value);
+        // unrolled LDS-broadcast steps: keep the scheduler from hoisting the
+        // next steps' LDS reads (it otherwise spills ~1 KB per lane)
+        if constexpr (ALG == 2) __builtin_amdgcn_sched_barrier(0);
+      });
+    } else {
+#pragma unroll 1
+      for (int kq = 0; kq < nk; ++kq) step(kq);
+    }
+  });
+  // rows of the block row -> U = d^-1/2 V, d of row q + 4r read from the
+  // diagonal (lane 17q + 4r); log-det and positivity from one lane per row
+  // (c == 0); the r row (last block, row 15) is left as it is
+  static_for<0, 4>([&](auto R) {
+    constexpr int r = decltype(R)::value;
+    const bool rrow = (bb == NB - 1 && r == 3) && q == 3;
+    const double dg = __shfl(blk(BBc)[r], 17 * q + 4 * r);
+    const double dv = rrow ? 1.0 : dg;
+    ok = ok && (dv > 0.0);
+    if (c == 0) ldet.add(dv);
+    const double rs = rrow ? 1.0 : rsqrt_nr(dv);
+    static_for<bb, NB>([&](auto JJ) { blk(JJ)[r] *= rs; });
+  });
+}
+
+// KEEP > 0 (correlated common process): only block rows 0..NB-KEEP-1 (the
+// pulsar's own columns) are factored; the trailing KEEP x KEEP blocks (the
+// common columns + r: their Schur complement S^G, d', rho) are written to
+// keep_out[((b - keep_b0) * keep_P + p)] as a dense (16 KEEP)^2 square, and
+// the unit term is the local part K - 1/2 log|Sigma_LL| - 1/2 log|phi_L|.
+template <int NB, int FULL, int W, int ALG = 0, int KEEP = 0>
+__global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(W, W)))
+void chol_mfma_kernel(const CholJob* __restrict__ jobs, int B, long long u0, int b_off,
+                      const double* __restrict__ theta, int ldth, double* __restrict__ out_units,
+                      double* __restrict__ keep_out, int keep_b0, int keep_P) {
+  constexpr int LD = 16 * NB;
+  using S = Split<NB>;
+  constexpr int H = S::H;
+  static_assert(NB - KEEP >= H, "kept blocks must lie in the phase-3 triangle");
+  __shared__ double phinv[LD];
+  __shared__ double rowbuf[ALG == 2 ? 2 * LD : 1];   // ALG 2: double-buffered row-k broadcast
+  const int lane = threadIdx.x;
+  const int q = lane >> 4, c = lane & 15;
+  const long long u = u0 + xcd_unit(blockIdx.x, gridDim.x);
+  const int p = (int)(u / B), b = (int)(u % B);
+  const CholJob J = jobs[p];
+  const double* A = J.mats + (long long)(b - b_off) * J.mstride;
+  const double* th = theta + (long long)b * ldth;
+
+  LogAcc lphi;
+  for (int a = lane; a < LD; a += 64) {
+    double pi = 0.0;
+    if (a < J.mreal) {
+      double ph = 0.0;
+      for (int e = J.col_ptr[a]; e < J.col_ptr[a + 1]; ++e) ph += spec_phi_body(J.spec[e], th);
+      pi = 1.0 / ph;
+      lphi.add(ph);
+    }
+    phinv[a] = pi;
+  }
+  const double lphi_sum = wave_sum(lphi.value());
+  __syncthreads();
+
+  auto load_block = [&](auto BI, auto BJ, v4d& v) {
+    constexpr int bi = decltype(BI)::value, bj = decltype(BJ)::value;
+    static_for<0, 4>([&](auto R) {
+      constexpr int r = decltype(R)::value;
+      v[r] = A[(long long)(16 * bi + q + 4 * r) * LD + 16 * bj + c];
+    });
+    if constexpr (bi == bj) {
+      const double pd = phinv[16 * bi + c];
+      static_for<0, 4>([&](auto R) {
+        constexpr int r = decltype(R)::value;
+        v[r] += (q + 4 * r == c) ? pd : 0.0;
+      });
+    }
+  };
+
+  LogAcc ldet;
+  bool ok = true;
+  // LDL^T panel row bb (ALG >= 1)
+  auto panel_ldl = [&](auto BBc, auto&& blk) {
+    panel_ldl_row<NB, FULL, ALG>(BBc, blk, q, c, ldet, ok, rowbuf);
+  };
+  // panel row bb over the blocks blk(j), j = bb..NB-1
+  auto panel = [&](auto BBc, auto&& blk) {
+    if constexpr (ALG >= 1) {
+      panel_ldl(BBc, blk);
+      return;
+    }
+    constexpr int bb = decltype(BBc)::value;
+    static_for<0, 4>([&](auto KR) {
+      constexpr int kr = decltype(KR)::value;
+      auto step = [&](const int kq) {
+        const int k = 4 * kr + kq;
+        const double piv = readlane_d(blk(BBc)[kr], 16 * kq + k);           // wave-uniform
+        ok = ok && (piv > 0.0);
+        ldet.add(piv);
+        const double rin = rsqrt_nr(piv);
+        const double sc = (q == kq) ? rin : 1.0;                             // scales row k only
+        const double xbb = blk(BBc)[kr] * sc;
+        // U[k][q + 4r] for this lane's rows; rows <= k are final (r < kr never
+        // changes, r == kr only for q > kq)
+        double ui[4];
+        static_for<kr, 4>([&](auto R) {
+          constexpr int r = decltype(R)::value;
+          const double v = __shfl(xbb, 16 * kq + q + 4 * r);
+          ui[r] = (r > kr || q > kq) ? v : 0.0;
+        });
+        double rk[NB];
+        static_for<bb, NB>([&](auto JJ) {
+          constexpr int j = decltype(JJ)::value;
+          const double x = (j == bb) ? xbb : blk(JJ)[kr] * sc;
+          blk(JJ)[kr] = x;
+          rk[j] = __shfl(x, 16 * kq + c);                                    // U[k][col c] of block (bb, j)
+        });
+        static_for<bb, NB>([&](auto JJ) {
+          constexpr int j = decltype(JJ)::value;
+          static_for<kr, 4>([&](auto R) {
+            constexpr int r = decltype(R)::value;
+            blk(JJ)[r] = fma(-ui[r], rk[j], blk(JJ)[r]);
+          });
+        });
+      };
+      constexpr int nk = (bb == NB - 1 && kr == 3) ? 3 : 4;   // the r column is not pivoted
+      if constexpr (FULL) {
+        static_for<0, nk>([&](auto KQ) { step(decltype(KQ)::value); });
+      } else {
+#pragma unroll 1
+        for (int kq = 0; kq < nk; ++kq) step(kq);
+      }
+    });
+  };
+
+  // ---- phase 1: block rows 0..H-1 ----
+  v4d U1[S::n1 > 0 ? S::n1 : 1];
+  static_for<0, H>([&](auto BI) {
+    constexpr int bi = decltype(BI)::value;
+    static_for<bi, NB>([&](auto BJ) { load_block(BI, BJ, U1[S::i1(bi, decltype(BJ)::value)]); });
+  });
+  static_for<0, H>([&](auto BBc) {
+    constexpr int bb = decltype(BBc)::value;
+    panel(BBc, [&](auto JJ) -> v4d& { return U1[S::i1(bb, decltype(JJ)::value)]; });
+    static_for<bb + 1, H>([&](auto II) {
+      constexpr int i = decltype(II)::value;
+      static_for<i, NB>([&](auto JJ) {
+        constexpr int j = decltype(JJ)::value;
+        syrk_update(U1[S::i1(i, j)], U1[S::i1(bb, i)], U1[S::i1(bb, j)]);
+      });
+    });
+  });
+  // ---- phase 2: A22 -= U12^T U12 ----
+  // block by block in row order: U1 column i is dead once row i of A22 is done
+  v4d U2[S::n2];
+  static_for<H, NB>([&](auto II) {
+    constexpr int i = decltype(II)::value;
+    static_for<i, NB>([&](auto JJ) {
+      constexpr int j = decltype(JJ)::value;
+      load_block(II, JJ, U2[S::i2(i, j)]);
+      static_for<0, H>([&](auto BBc) {
+        constexpr int bb = decltype(BBc)::value;
+        syrk_update(U2[S::i2(i, j)], U1[S::i1(bb, i)], U1[S::i1(bb, j)]);
+      });
+    });
+  });
+  // ---- phase 3: factor A22 (up to the kept blocks) ----
+  static_for<H, NB - KEEP>([&](auto BBc) {
+    constexpr int bb = decltype(BBc)::value;
+    panel(BBc, [&](auto JJ) -> v4d& { return U2[S::i2(bb, decltype(JJ)::value)]; });
+    static_for<bb + 1, NB>([&](auto II) {
+      constexpr int i = decltype(II)::value;
+      static_for<i, NB>([&](auto JJ) {
+        constexpr int j = decltype(JJ)::value;
+        syrk_update(U2[S::i2(i, j)], U2[S::i2(bb, i)], U2[S::i2(bb, j)]);
+      });
+    });
+  });
+  double qv = 0.0;
+  if constexpr (KEEP == 0) {
+    qv = readlane_d(U2[S::i2(NB - 1, NB - 1)][3], 63);
+  } else {
+    constexpr int KD = 16 * KEEP;
+    double* ko = keep_out + ((long long)(b - keep_b0) * keep_P + p) * (KD * KD);
+    static_for<NB - KEEP, NB>([&](auto II) {
+      constexpr int i = decltype(II)::value;
+      static_for<i, NB>([&](auto JJ) {
+        constexpr int j = decltype(JJ)::value;
+        static_for<0, 4>([&](auto RR) {
+          constexpr int r = decltype(RR)::value;
+          const int row = 16 * (i - (NB - KEEP)) + q + 4 * r, col = 16 * (j - (NB - KEEP)) + c;
+          const double v = U2[S::i2(i, j)][r];
+          if (i != j || row <= col) {
+            ko[row * KD + col] = v;
+            ko[col * KD + row] = v;
+          }
+        });
+      });
+    });
+  }
+  double ldet_v = ldet.value();
+  bool ok_all = ok;
+  if constexpr (ALG >= 1) {          // per-lane partial log-dets and checks
+    ldet_v = wave_sum(ldet_v);
+    ok_all = __all(ok);
+  }
+  if (lane == 0) {
+    double lnl = J.K[(long long)(b - b_off) * J.kstride] - 0.5 * qv - 0.5 * ldet_v - 0.5 * lphi_sum;
+    if (!ok_all || J.fail) lnl = -INFINITY;
+    out_units[(long long)p * B + b] = lnl;
+  }
+}
+
+// ----------------------------------------------------------------------------
+// batched factorisation for wide bases (NB > 9, e.g. C4's 193-wide Sigma):
+// one wave per unit, LEFT-looking over block rows.  Block row i (<= NB
+// blocks, C/D layout) is loaded into registers, takes the updates
+// A_ij -= U_pi^T U_pj of every finished row p < i (4 MFMAs per block, the U
+// blocks streamed back from a per-wave scratch in the same lane layout,
+// double-buffered), is factored by the LDL^T panel and written to scratch.
+// Same arithmetic as chol_mfma_kernel (right-looking), re-ordered.
+// ----------------------------------------------------------------------------
+constexpr int BIG_NB_MAX = 16;
+
+template <int NB>
+__device__ __forceinline__ long long big_blk(int p, int j) {   // packed upper block index
+  return (long long)p * NB - (long long)p * (p - 1) / 2 + (j - p);
+}
+
+template <int NB>
+__global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(1, 1)))
+void chol_big_kernel(const CholJob* __restrict__ jobs, int B, long long u0, int b_off,
+                     const double* __restrict__ theta, int ldth, double* __restrict__ out_units,
+                     double* __restrict__ scratch) {
+  constexpr int LD = 16 * NB;
+  __shared__ double phinv[LD];
+  const int lane = threadIdx.x;
+  const int q = lane >> 4, c = lane & 15;
+  const long long u = u0 + xcd_unit(blockIdx.x, gridDim.x);
+  const int p = (int)(u / B), b = (int)(u % B);
+  const CholJob J = jobs[p];
+  const double* A = J.mats + (long long)(b - b_off) * J.mstride;
+  const double* th = theta + (long long)b * ldth;
+  double* scr = scratch + (long long)blockIdx.x * (NB * (NB + 1) / 2) * 256 + lane * 4;
+
+  LogAcc lphi;
+  for (int a = lane; a < LD; a += 64) {
+    double pi = 0.0;
+    if (a < J.mreal) {
+      double ph = 0.0;
+      for (int e = J.col_ptr[a]; e < J.col_ptr[a + 1]; ++e) ph += spec_phi_body(J.spec[e], th);
+      pi = 1.0 / ph;
+      lphi.add(ph);
+    }
+    phinv[a] = pi;
+  }
+  const double lphi_sum = wave_sum(lphi.value());
+  __syncthreads();
+
+  LogAcc ldet;
+  bool ok = true;
+  double qv = 0.0;
+  static_for<0, NB>([&](auto I) {
+    constexpr int i = decltype(I)::value;
+    constexpr int W = NB - i;                       // blocks in row i
+    v4d R[W];
+    static_for<0, W>([&](auto JJ) {
+      constexpr int j = i + decltype(JJ)::value;
+      static_for<0, 4>([&](auto RR) {
+        constexpr int r = decltype(RR)::value;
+        R[j - i][r] = A[(long long)(16 * i + q + 4 * r) * LD + 16 * j + c];
+      });
+      if constexpr (j == i) {
+        const double pd = phinv[16 * i + c];
+        static_for<0, 4>([&](auto RR) {
+          constexpr int r = decltype(RR)::value;
+          R[0][r] += (q + 4 * r == c) ? pd : 0.0;
+        });
+      }
+    });
+    if constexpr (i > 0) {
+      // U blocks (p, i..NB-1) of earlier rows: Ui once, then each Uj in turn
+      // (the compiler issues the row's loads ahead of its MFMAs)
+#pragma unroll 1
+      for (int pp = 0; pp < i; ++pp) {
+        const v4d Ui = *(const v4d*)(scr + big_blk<NB>(pp, i) * 256);
+        static_for<0, W>([&](auto JJ) {
+          constexpr int jj = decltype(JJ)::value;
+          const v4d Uj = *(const v4d*)(scr + big_blk<NB>(pp, i + jj) * 256);
+          syrk_update(R[jj], Ui, Uj);
+        });
+      }
+    }
+    panel_ldl_row<NB, 0, 1>(I, [&](auto JJ) -> v4d& { return R[decltype(JJ)::value - i]; }, q, c, ldet, ok,
+                            nullptr);
+    if constexpr (i < NB - 1) {
+      static_for<0, W>([&](auto JJ) {
+        constexpr int j = i + decltype(JJ)::value;
+        *(v4d*)(scr + big_blk<NB>(i, j) * 256) = R[j - i];
+      });
+    } else {
+      qv = readlane_d(R[0][3], 63);
+    }
+  });
+  const double ldet_v = wave_sum(ldet.value());
+  const bool ok_all = __all(ok);
+  if (lane == 0) {
+    double lnl = J.K[(long long)(b - b_off) * J.kstride] - 0.5 * qv - 0.5 * ldet_v - 0.5 * lphi_sum;
+    if (!ok_all || J.fail) lnl = -INFINITY;
+    out_units[(long long)p * B + b] = lnl;
+  }
+}
+
+// ----------------------------------------------------------------------------
+// correlated common process (HD / monopole / dipole ORF; [ent]
+// FourierBasisCommonGP, enterprise_models.py:390-415), fixed white noise.
+// Per sample b (after the per-pulsar partial factorisations):
+//   M_g = Gamma phi_c(g) + diag_a(phi_own(a, g))          (P x P, per common column g)
+//   Sigma_c = blockdiag_a(S^G_a) + [M_g^-1]_(a,g),(b,g)    (P n_c square, + r row)
+//   lnL_b = sum_a local_a - 1/2 (log|Sigma_c| + q_c + sum_g log|M_g|)
+// Sigma_c is factored densely (blocked right-looking, 64-wide panels: diagonal
+// block by LDS Cholesky + explicit inverse, panel and trailing update by fp64
+// MFMA); its last pivot is q_c = rho - d'^T Sigma_c^-1 d'.
+// ----------------------------------------------------------------------------
+struct CommonPsr {
+  const int* colptr;     // reduced-layout CSR of the pulsar's own spectral entries
+  const DSpec* spec;
+  int gstart;            // reduced index of common column 0
+  int pad_;
+};
+
+constexpr int DCB = 64;            // dense panel width
+
+
+// ---- launchers defined in the other translation units ----------------------
+// each returns 0 on success (negative EWH_E* on error)
+int launch_contract_nb(int nb, const PsrDev& P, const double* w, const double* beta, const double* s,
+                       const double* fac, double* G, int nb_samples, hipStream_t st);
+int launch_contract2_nb(int nb, const PsrDev& P, const double* w, const double* beta, double* s,
+                        long long s_stride, double* G, int nb_samples, hipStream_t st);
+// mode: ewh_set_kernel_mode; returns 1 if no register kernel applies (caller falls back)
+int launch_chol_small(int mode, int nb, const CholJob* jobs, int B, long long u0, long long n, int b_off,
+                      const double* theta, int ldth, double* units, hipStream_t st);
+int launch_chol_big_nb(int nb, const CholJob* jobs, int B, long long u0, long long n, int b_off,
+                       const double* theta, int ldth, double* units, double* scr, long long cap, hipStream_t st);
+int launch_partial_nb(int nb, int keep, const CholJob* jobs, int B, long long u0, long long n,
+                      const double* theta, int ldth, double* units, double* keep_out, int P, hipStream_t st);
+
+}  // namespace ewh_dev

@@ -294,7 +294,7 @@ def interpret_white_noise_prior(prior):
 
 
 def hd_orf(pos1, pos2):
-    """[ent] utils.hd_orf (kept for the correlated path, next round)."""
+    """[ent] utils.hd_orf (enterprise_models.py:397)."""
     if np.all(pos1 == pos2):
         return 1.0
     omc2 = (1 - np.dot(pos1, pos2)) / 2
@@ -307,3 +307,28 @@ def hd_orf_noauto(pos1, pos2):
         return 0.0
     omc2 = (1 - np.dot(pos1, pos2)) / 2
     return 1.5 * omc2 * np.log(omc2) - 0.25 * omc2 + 0.5
+
+
+def monopole_orf(pos1, pos2):
+    """[ent] utils.monopole_orf (enterprise_models.py:405); the 1e-5 on the
+    auto term keeps Gamma invertible (enterprise's regularisation)."""
+    return 1.0 + 1e-5 if np.all(pos1 == pos2) else 1.0
+
+
+def dipole_orf(pos1, pos2):
+    """[ent] utils.dipole_orf (enterprise_models.py:411)."""
+    return 1.0 + 1e-5 if np.all(pos1 == pos2) else float(np.dot(pos1, pos2))
+
+
+ORFS = {"hd": hd_orf, "hd_noauto": hd_orf_noauto, "monopole": monopole_orf, "dipole": dipole_orf}
+
+
+def orf_matrix(kind, positions):
+    """Gamma_ab = orf(pos_a, pos_b) over the PTA's pulsars (diagonal included)."""
+    f = ORFS[kind]
+    P = len(positions)
+    G = np.empty((P, P))
+    for a in range(P):
+        for b in range(P):
+            G[a, b] = f(np.asarray(positions[a], float), np.asarray(positions[b], float))
+    return G

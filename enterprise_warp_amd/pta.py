@@ -167,6 +167,50 @@ class PTA:
         return all(isinstance(p, parameter.ConstantParameter)
                    for c in self._collections for w in c.white for p in w.params)
 
+    def correlated(self):
+        """True if the model has a spatially correlated common process
+        (FourierBasisCommonGP with an ORF, enterprise_models.py:390-415)."""
+        return any(c.common is not None for c in self._collections)
+
+    def common_layout(self):
+        """ORF matrix and spectral entries of the correlated common process;
+        checks that every pulsar carries it with the same frequencies."""
+        from .models import orf_matrix
+        cs = [c.common for c in self._collections]
+        if any(c is None for c in cs):
+            raise ValueError("a correlated common process must be present in every pulsar")
+        ref = cs[0]
+        for c in cs[1:]:
+            if c["orf"] != ref["orf"] or len(c["cols"]) != len(ref["cols"]) or \
+                    not np.allclose([e["f"] for e in c["entries"]], [e["f"] for e in ref["entries"]], rtol=0, atol=0):
+                raise ValueError("the correlated common process differs between pulsars (ORF, Tspan or nfreqs)")
+        spec = []
+        for g, e in enumerate(ref["entries"]):
+            spec.append(self._spec_tuple(e, g))
+        G = orf_matrix(ref["orf"], [c.psr.pos for c in self._collections])
+        return {"orf": np.ascontiguousarray(G), "spec": spec, "n_col": len(ref["cols"]), "kind": ref["orf"]}
+
+    def _spec_tuple(self, e, j):
+        if e["kind"] == "const":
+            return (_lib.SPEC_CONST, j, (-1, e["value"]), (-1, 0.0), (-1, 0.0), 0.0, 0.0)
+        if e["kind"] == "powerlaw":
+            pa = e["pars"]
+            return (_lib.SPEC_POWERLAW, j, self._pref(pa["log10_A"]), self._pref(pa["gamma"]), (-1, 0.0),
+                    e["f"], e["df"])
+        if e["kind"] == "turnover":
+            pa = e["pars"]
+            return (_lib.SPEC_TURNOVER, j, self._pref(pa["log10_A"]), self._pref(pa["gamma"]),
+                    self._pref(pa["fc"]), e["f"], e["df"])
+        if e["kind"] == "free_spectrum":
+            p = e["pars"]["log10_rho"]
+            if isinstance(p, parameter.ConstantParameter):
+                vals = np.atleast_1d(p.value)
+                ref = (-1, float(vals[e["mode"]] if len(vals) > 1 else vals[0]))
+            else:
+                ref = self._pref(p, e["mode"])
+            return (_lib.SPEC_FREESPEC, j, ref, (-1, 0.0), (-1, 0.0), e["f"], 0.0)
+        raise ValueError(e["kind"])
+
     def basis_varies(self):
         """True if some basis depends on theta (chromred 'vary'): no TNT cache."""
         return any(c.basis_groups for c in self._collections)
@@ -174,6 +218,7 @@ class PTA:
     def layout(self):
         """Host-side per-pulsar tables for the engine (plain numpy)."""
         out = []
+        corr = self.correlated()
         for c in self._collections:
             psr = c.psr
             n = len(psr.toas)
@@ -199,32 +244,30 @@ class PTA:
             ep_start = np.array([e[0] for e in eps], np.int32)
             ep_stop = np.array([e[1] for e in eps], np.int32)
             ep_slot = np.array([slot(e[2]) for e in eps], np.int32)
+            # column order: [leading constant-phi | own | common (g order)] when the
+            # PTA has a correlated common process (the device keeps the common
+            # block for the cross-pulsar factorisation, include/ewarp_hip.h)
+            m = c.T.shape[1]
+            ncom = 0
+            order = np.arange(m)
+            if corr:
+                com = list(c.common["cols"])
+                if any(j < c.n_lead_const for j in com) or len(set(com)) != len(com):
+                    raise ValueError(f"{c.name}: common columns overlap the timing model or each other")
+                own = [j for j in range(m) if j not in set(com)]
+                order = np.array(own + com)
+                ncom = len(com)
+            pos = np.empty(m, int)
+            pos[order] = np.arange(m)
             spec = []
             for j, ents in enumerate(c.entries):
                 for e in ents:
-                    if e["kind"] == "const":
-                        spec.append((_lib.SPEC_CONST, j, (-1, e["value"]), (-1, 0.0), (-1, 0.0), 0.0, 0.0))
-                    elif e["kind"] == "powerlaw":
-                        pa = e["pars"]
-                        spec.append((_lib.SPEC_POWERLAW, j, self._pref(pa["log10_A"]), self._pref(pa["gamma"]),
-                                     (-1, 0.0), e["f"], e["df"]))
-                    elif e["kind"] == "turnover":
-                        pa = e["pars"]
-                        spec.append((_lib.SPEC_TURNOVER, j, self._pref(pa["log10_A"]), self._pref(pa["gamma"]),
-                                     self._pref(pa["fc"]), e["f"], e["df"]))
-                    elif e["kind"] == "free_spectrum":
-                        p = e["pars"]["log10_rho"]
-                        if isinstance(p, parameter.ConstantParameter):
-                            vals = np.atleast_1d(p.value)
-                            ref = (-1, float(vals[e["mode"]] if len(vals) > 1 else vals[0]))
-                        else:
-                            ref = self._pref(p, e["mode"])
-                        spec.append((_lib.SPEC_FREESPEC, j, ref, (-1, 0.0), (-1, 0.0), e["f"], 0.0))
-                    else:
-                        raise ValueError(e["kind"])
+                    if e.get("common"):
+                        continue                      # in the PTA's common descriptor
+                    spec.append(self._spec_tuple(e, int(pos[j])))
             bgroups = [self._pref(p) for p in c.basis_groups]
-            out.append(dict(name=c.name, T=np.ascontiguousarray(c.T, dtype=float),
-                            bgroups=bgroups, col_bgroup=np.ascontiguousarray(c.col_bgroup, np.int32),
+            out.append(dict(name=c.name, T=np.ascontiguousarray(c.T[:, order], dtype=float), n_common=ncom,
+                            bgroups=bgroups, col_bgroup=np.ascontiguousarray(c.col_bgroup[order], np.int32),
                             ln_chrom=np.ascontiguousarray(c.ln_chrom, dtype=float),
                             resid=np.ascontiguousarray(psr.residuals, dtype=float),
                             toaerr=np.ascontiguousarray(psr.toaerrs, dtype=float),
@@ -287,9 +330,22 @@ class Engine:
                 len(L["slots"]), slots, _as_ptr(L["efac"], C.c_int32), _as_ptr(L["equad"], C.c_int32),
                 len(L["ep_start"]), _as_ptr(L["ep_start"], C.c_int32), _as_ptr(L["ep_stop"], C.c_int32),
                 _as_ptr(L["ep_slot"], C.c_int32), spec,
-                len(L["bgroups"]), bg, _as_ptr(L["col_bgroup"], C.c_int32), _as_ptr(L["ln_chrom"], C.c_double))
+                len(L["bgroups"]), bg, _as_ptr(L["col_bgroup"], C.c_int32), _as_ptr(L["ln_chrom"], C.c_double),
+                L["n_common"])
         self.white_fixed = pta.white_fixed() and not pta.basis_varies()
-        d = _lib.PtaDesc(_lib.EWH_ABI_VERSION, len(lay), self.n_param, int(self.white_fixed), descs)
+        common = None
+        self.correlated = pta.correlated()
+        if self.correlated:
+            cl = pta.common_layout()
+            cspec = (_lib.SpecEntry * cl["n_col"])()
+            for k, (kind, col, p0, p1, p2, f, df) in enumerate(cl["spec"]):
+                cspec[k] = _lib.SpecEntry(kind, col, _lib.Pref(p0[0], 0, p0[1]), _lib.Pref(p1[0], 0, p1[1]),
+                                          _lib.Pref(p2[0], 0, p2[1]), f, df, const.fyr)
+            keep.extend([cl["orf"], cspec])
+            common = _lib.CommonDesc(cl["n_col"], _as_ptr(cl["orf"], C.c_double), cspec)
+            keep.append(common)
+        d = _lib.PtaDesc(_lib.EWH_ABI_VERSION, len(lay), self.n_param, int(self.white_fixed), descs,
+                         C.pointer(common) if common is not None else None)
         h = C.c_void_p()
         _lib.check(self.lib.ewh_create(C.byref(d), int(device), C.byref(h)))
         self.h = h

@@ -241,10 +241,6 @@ class _GP(Signal):
         self.orf = orf
 
     def __call__(self, psr):
-        if self.orf is not None:
-            raise NotImplementedError(
-                "spatially correlated common process (FourierBasisCommonGP: hd/mono/dipole ORF) is the next "
-                "row of SURVEY.md §8(f); this round's device path covers uncorrelated and CURN models")
         return _BoundGP(self, psr)
 
 
@@ -255,6 +251,7 @@ class _BoundGP:
         self.name = sig.name
         self.spectrum = sig.spectrum
         self.basis_spec = sig.basis
+        self.orf = sig.orf          # None, or the ORF of a correlated common process
         masks = sig.selection.masks(psr)
         self.sel_flag = getattr(sig.selection.func, "flag", None)
         self.sel_value = getattr(sig.selection.func, "value", None)
@@ -299,6 +296,8 @@ class _BoundGP:
                     d["pnames"][loc] = p.name
             if part["basis_par"] is not None:
                 d["idx_param"] = part["basis_par"].name
+            if self.orf is not None:
+                d["orf"] = self.orf
             out.append(d)
         return out
 
@@ -346,6 +345,7 @@ class SignalCollection:
         entries = []       # per column: list of entry dicts
         by_hash = {}       # column bytes -> candidate indices (same result as a linear np.array_equal scan)
         self.col_bgroup_map = {}   # column -> chromatic-index Parameter (theta-dependent basis)
+        self.common = None         # correlated common process: {"name", "orf", "cols", "entries"}
         self.n_tm = 0
         seen_gp = False
 
@@ -369,12 +369,24 @@ class SignalCollection:
             elif isinstance(b, _BoundGP):
                 seen_gp = True
                 comp = b.spectrum.components
+                if b.orf is not None:
+                    if self.common is not None:
+                        raise NotImplementedError(f"{psr.name}: more than one correlated common process")
+                    if len(b.parts) != 1 or b.parts[0]["basis_par"] is not None:
+                        raise NotImplementedError("a correlated common process must be one unselected Fourier basis")
+                    self.common = {"name": b.name, "orf": b.orf, "cols": [], "entries": []}
                 for part in b.parts:
                     f = part["f"]
                     df = np.repeat(np.diff(np.concatenate((np.array([0]), f[::comp]))), comp)
                     for j in range(part["F"].shape[1]):
                         e = {"kind": b.spectrum.kind, "pars": part["pars"], "f": f[j], "df": df[j], "mode": j // 2}
-                        if part["basis_par"] is None:
+                        if b.orf is not None:
+                            # [ent] FourierBasisCommonGP: phi(a, a) = orf(a, a) phi_c on the
+                            # merged column; cross-pulsar terms in the PTA's common block
+                            e["common"] = True
+                            self.common["cols"].append(add(part["F"][:, j], e))
+                            self.common["entries"].append(e)
+                        elif part["basis_par"] is None:
                             add(part["F"][:, j], e)
                         else:   # theta-dependent basis: own column, never merged
                             cols.append(part["F"][:, j])

@@ -170,7 +170,7 @@ def simulate_residuals(pta, values, seed):
         phi = np.zeros(c.T.shape[1])
         for j, ents in enumerate(c.entries):
             for e in ents:
-                if e["kind"] == "const":
+                if e["kind"] == "const" or e.get("common"):
                     continue
                 vals = {k: values[p.name] if p.value is None else p.value for k, p in e["pars"].items()}
                 if e["kind"] == "free_spectrum":
@@ -179,6 +179,23 @@ def simulate_residuals(pta, values, seed):
                     phi[j] += _spec_single(e["kind"], e["f"], e["df"], vals)
         r += c.T @ (np.sqrt(phi) * rng.standard_normal(len(phi)))
         psr.residuals = r
+    if pta.correlated():
+        # the common process: per column g, coefficients ~ N(0, Gamma phi_c(g))
+        # across pulsars (Gamma from the ORF; a singular Gamma, e.g. HD
+        # without auto terms, falls back to its eigen-square-root)
+        cl = pta.common_layout()
+        w, V = np.linalg.eigh(cl["orf"])
+        Lg = V * np.sqrt(np.clip(w, 0, None))[None, :]
+        cols = [c.common["cols"] for c in pta.signal_collections]
+        for g, e in enumerate(pta.signal_collections[0].common["entries"]):
+            vals = {k: values[p.name] if p.value is None else p.value for k, p in e["pars"].items()}
+            if e["kind"] == "free_spectrum":
+                ph = 10 ** (2 * np.atleast_1d(vals["log10_rho"])[e["mode"]])
+            else:
+                ph = _spec_single(e["kind"], e["f"], e["df"], vals)
+            z = Lg @ rng.standard_normal(len(cols)) * np.sqrt(ph)
+            for a, c in enumerate(pta.signal_collections):
+                c.psr.residuals = c.psr.residuals + c.T[:, cols[a][g]] * z[a]
     pta._drop_engine()
 
 
@@ -280,6 +297,27 @@ def config_c4(n_psr=30, n_min=1000, n_max=12000, seed=30, epoch_size=16):
     truth = truth_values(pta, seed + 2, white=wn)
     simulate_residuals(pta, truth, seed + 3)
     return SimpleNamespace(name="C4", pta=pta, truth=truth, B=1024, theta_seed=seed)
+
+
+def config_c5(n_psr=100, n_toa=20000, seed=100, epoch_size=16, gwb="hd_vary_gamma_14_nfreqs", nfreqs=30):
+    """BASELINE config 5: n_psr x n_toa PTA, fixed white noise + ECORR, red and
+    DM noise, and a Hellings-Downs correlated GWB (cross-pulsar Sigma)."""
+    rng = np.random.default_rng(seed)
+    psrs = []
+    for i in range(n_psr):
+        v = rng.standard_normal(3)
+        psrs.append(make_pulsar(f"J{i:04d}+{seed:04d}", int(n_toa), seed=seed * 1000 + i, pos=v / np.linalg.norm(v),
+                                epoch_size=epoch_size))
+    Tspan = max(p.toas.max() for p in psrs) - min(p.toas.min() for p in psrs)
+    ns = params_namespace(Tspan, True)
+    wn = white_noisedict(psrs, seed + 1)
+    terms = {"efac": "by_backend", "equad": "by_backend", "ecorr": "by_backend",
+             "spin_noise": f"powerlaw_{nfreqs}_nfreqs", "dm_noise": f"powerlaw_{nfreqs}_nfreqs"}
+    pta = build_pta(psrs, terms, {"gwb": gwb}, ns, wn)
+    truth = truth_values(pta, seed + 2, white=wn)
+    simulate_residuals(pta, truth, seed + 3)
+    return SimpleNamespace(name="C5", pta=pta, truth=truth, B=256, theta_seed=seed, terms=terms,
+                           common={"gwb": gwb})
 
 
 def config_c1(data_dir, noise_json=None, seed=1832):

@@ -49,7 +49,7 @@
 extern "C" {
 #endif
 
-#define EWH_ABI_VERSION 2
+#define EWH_ABI_VERSION 3
 
 enum ewh_status {
   EWH_OK = 0,
@@ -117,7 +117,25 @@ typedef struct ewh_pulsar_desc {
   const ewh_pref* bgroup_idx;   /* n_bgroup */
   const int32_t* col_bgroup;    /* n_col (-1: fixed column); NULL if n_bgroup == 0 */
   const double* ln_chrom;       /* n_toa: ln(1400 MHz / nu_t); NULL if n_bgroup == 0 */
+  /* correlated common process (ewh_pta_desc.common != NULL): the LAST
+   * n_common basis columns are the common signal's columns, in the common
+   * order g = 0..n_common-1 (after the leading constant-phi columns and the
+   * pulsar's other columns).  Their spec entries here are the pulsar's own
+   * signals merged onto them (e.g. red noise); the common signal's own phi is
+   * in ewh_common_desc. 0 when uncorrelated. */
+  int32_t n_common;
 } ewh_pulsar_desc;
+
+/* A spatially correlated common process ([ent] FourierBasisCommonGP with an
+ * ORF: enterprise_models.py:390-415): Phi couples column g of pulsar a with
+ * column g of pulsar b by orf[a][b] * phi_common(g); the pulsars' own
+ * signals add to the diagonal.  Requires fixed white noise (this ABI
+ * version). */
+typedef struct ewh_common_desc {
+  int32_t n_col;                /* common columns per pulsar (2 x frequencies), <= 31 */
+  const double* orf;            /* n_pulsar x n_pulsar, row-major: Gamma_ab (diagonal included) */
+  const ewh_spec_entry* spec;   /* n_col entries, spec[g].col = g: phi_common of column g */
+} ewh_common_desc;
 
 typedef struct ewh_pta_desc {
   int32_t abi_version;    /* EWH_ABI_VERSION */
@@ -125,6 +143,7 @@ typedef struct ewh_pta_desc {
   int32_t n_param;        /* theta row length */
   int32_t white_fixed;    /* 1: no white-noise slot references theta -> cache TNT */
   const ewh_pulsar_desc* pulsars;
+  const ewh_common_desc* common;   /* NULL: uncorrelated / CURN (per-pulsar Sigma) */
 } ewh_pta_desc;
 
 typedef struct ewh_handle ewh_handle;
@@ -136,7 +155,9 @@ int ewh_create(const ewh_pta_desc* desc, int device, ewh_handle** out);
 int ewh_lnl_batch(ewh_handle* h, const double* theta_host, int32_t B, double* out_host);
 
 /* Device variant on a contiguous range [unit_begin, unit_end) of units
- * u = pulsar * B + sample.  out_dev[b] = sum of the unit lnL terms of sample
+ * u = pulsar * B + sample.  With a correlated common process the range must
+ * be the whole batch [0, n_pulsar * B) (shard samples across devices by
+ * passing each one its own theta rows instead).  out_dev[b] = sum of the unit lnL terms of sample
  * b inside the range (0 where the range has none).  Asynchronous on `stream`
  * (a hipStream_t; NULL = the default stream).  theta_dev and out_dev are
  * device pointers. */

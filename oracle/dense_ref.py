@@ -52,3 +52,57 @@ def woodbury_lnl(oracle_pulsar, params, tm_var=None):
     expval = sl.cho_solve(cf, TNr)
     return (-0.5 * (rNr + ldN)
             + 0.5 * (TNr @ expval - 2 * np.sum(np.log(np.diag(cf[0]))) - np.sum(np.log(phi))))
+
+
+def dense_lnl_pta(oracle_pta, params, tm_var):
+    """lnL of a whole (possibly correlated) PTA from the dense covariance
+    C = blockdiag_a(N_a) + T Phi T^T over all TOAs, with Phi the global prior
+    (cross-pulsar ORF terms included) and a finite timing-model variance."""
+    o = oracle_pta
+    Phi, off = o.phi_global(params)
+    for a, pp in enumerate(o.pulsars):
+        for g in pp.gps:
+            if g["kind"] == "tm":
+                ix = off[a] + np.asarray(g["idx"])
+                Phi[ix, ix] = tm_var
+    ns = [len(pp.r) for pp in o.pulsars]
+    toff = np.concatenate(([0], np.cumsum(ns)))
+    n = toff[-1]
+    C = np.zeros((n, n))
+    T = np.zeros((n, off[-1]))
+    r = np.concatenate([pp.r for pp in o.pulsars])
+    for a, pp in enumerate(o.pulsars):
+        D, ep = pp._sm(params)
+        sl_ = slice(toff[a], toff[a + 1])
+        C[sl_, sl_] = np.diag(D)
+        for slc, jv in ep:
+            s0, s1 = toff[a] + slc.start, toff[a] + slc.stop
+            C[s0:s1, s0:s1] += jv
+        T[sl_, off[a]:off[a + 1]] = pp.basis(params)
+    C += T @ Phi @ T.T
+    cf = sl.cho_factor(C, lower=True)
+    x = sl.cho_solve(cf, r)
+    return -0.5 * np.dot(r, x) - np.sum(np.log(np.diag(cf[0])))
+
+
+def woodbury_lnl_pta(oracle_pta, params, tm_var):
+    """The enterprise route (Sigma = blockdiag(TNT) + Phi^-1) with the same
+    finite timing-model variance, for comparison with dense_lnl_pta."""
+    o = oracle_pta
+    Phi, off = o.phi_global(params)
+    for a, pp in enumerate(o.pulsars):
+        for g in pp.gps:
+            if g["kind"] == "tm":
+                ix = off[a] + np.asarray(g["idx"])
+                Phi[ix, ix] = tm_var
+    Phiinv = np.linalg.inv(Phi)
+    _, logdet_phi = np.linalg.slogdet(Phi)
+    terms = [pp.white_terms(params) for pp in o.pulsars]
+    S = Phiinv.copy()
+    for a, t in enumerate(terms):
+        S[off[a]:off[a + 1], off[a]:off[a + 1]] += t[0]
+    d = np.concatenate([t[1] for t in terms])
+    cf = sl.cho_factor(S)
+    x = sl.cho_solve(cf, d)
+    return (-0.5 * sum(t[2] + t[3] for t in terms)
+            + 0.5 * (d @ x - 2 * np.sum(np.log(np.diag(cf[0]))) - logdet_phi))

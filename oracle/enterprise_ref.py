@@ -32,6 +32,24 @@ FYR = 1.0 / YR                     # [ent] constants.fyr
 
 
 # --------------------------------------------------------------------------
+# overlap reduction functions ([ent] utils.hd_orf / monopole_orf / dipole_orf;
+# hd_orf_noauto from the reference, enterprise_models.py:565-572)
+# --------------------------------------------------------------------------
+def orf_value(kind, pos1, pos2):
+    same = np.all(pos1 == pos2)
+    if kind in ("hd", "hd_noauto"):
+        if same:
+            return 1.0 if kind == "hd" else 0.0
+        omc2 = (1 - np.dot(pos1, pos2)) / 2
+        return 1.5 * omc2 * np.log(omc2) - 0.25 * omc2 + 0.5
+    if kind == "monopole":
+        return 1.0 + 1e-5 if same else 1.0
+    if kind == "dipole":
+        return 1.0 + 1e-5 if same else float(np.dot(pos1, pos2))
+    raise ValueError(kind)
+
+
+# --------------------------------------------------------------------------
 # bases and spectra
 # --------------------------------------------------------------------------
 def fourier_basis(toas, nmodes, Tspan):
@@ -241,7 +259,8 @@ class OraclePulsar:
                 else:
                     names[p] = ("name", pname(self.name, t["name"], key, p))
             out.append({"kind": "gp", "idx": idx, "f": Ff, "spectrum": t["spectrum"],
-                        "names": names, "components": int(t.get("components", 2))})
+                        "names": names, "components": int(t.get("components", 2)),
+                        "orf": t.get("orf"), "name": t["name"]})
         return out
 
     # ---- parameters -------------------------------------------------------
@@ -267,12 +286,29 @@ class OraclePulsar:
             raise ValueError("model has no MeasurementNoise term")
         return nd
 
+    def gp_values(self, g, params):
+        """phi of one GP signal on its own columns (before merging)."""
+        nm = g["names"]
+        if g["spectrum"] == "powerlaw":
+            return powerlaw(g["f"], self._val(params, nm["log10_A"]), self._val(params, nm["gamma"]),
+                            g["components"])
+        if g["spectrum"] == "turnover":
+            return powerlaw_bpl(g["f"], self._val(params, nm["log10_A"]), self._val(params, nm["gamma"]),
+                                self._val(params, nm["fc"]), g["components"])
+        return free_spectrum(g["f"], self._val(params, nm["log10_rho"]))
+
     def phi(self, params):
-        """[ent] SignalCollection.get_phi: per-column sum over merged signals."""
+        """[ent] SignalCollection.get_phi: per-column sum over merged signals;
+        a common (ORF) signal contributes orf(pos, pos) * phi_gw on its columns
+        ([ent] FourierBasisCommonGP.get_phi)."""
         phi = np.zeros(self.T.shape[1])
         for g in self.gps:
             if g["kind"] == "tm":
                 phi[g["idx"]] += 1e40                      # [ent] utils.tm_prior
+                continue
+            if g.get("orf"):
+                pos = np.asarray(self.psr.pos, float)
+                phi[g["idx"]] += orf_value(g["orf"], pos, pos) * self.gp_values(g, params)
                 continue
             nm = g["names"]
             if g["spectrum"] == "powerlaw":
@@ -351,8 +387,10 @@ class OraclePulsar:
 
 
 class OraclePTA:
-    """Restates [ent] signal_base.PTA + LogLikelihood.__call__ (uncorrelated /
-    CURN path: `pta._commonsignals` empty), reached at bilby_warp.py:35.
+    """Restates [ent] signal_base.PTA + LogLikelihood.__call__, reached at
+    bilby_warp.py:35: the per-pulsar path (uncorrelated / CURN,
+    `pta._commonsignals` empty) and the correlated one (HD / monopole / dipole
+    ORF, FourierBasisCommonGP at enterprise_models.py:390-415).
 
     `fixed_white=True` mimics enterprise's cache_call: TNT / TNr / rNr /
     log|N| are computed once (white-noise parameters are Constants)."""
@@ -363,7 +401,83 @@ class OraclePTA:
         if fixed_params is not None and not any(pp.basis_params for pp in self.pulsars):
             self.fixed = [pp.white_terms(fixed_params) for pp in self.pulsars]
 
+    def correlated(self):
+        return any(g.get("orf") for pp in self.pulsars for g in pp.gps)
+
+    def phi_global(self, params):
+        """[ent] PTA.get_phi for a correlated common signal: block-diagonal
+        per-pulsar phi plus Phi[(a, col_a(j)), (b, col_b(j))] = orf(a, b) *
+        phi_common(j) for a != b (get_phicross), as one dense matrix."""
+        sizes = [pp.T.shape[1] for pp in self.pulsars]
+        off = np.concatenate(([0], np.cumsum(sizes)))
+        Phi = np.zeros((off[-1], off[-1]))
+        for a, pp in enumerate(self.pulsars):
+            Phi[np.arange(off[a], off[a + 1]), np.arange(off[a], off[a + 1])] = pp.phi(params)
+        commons = {}
+        for a, pp in enumerate(self.pulsars):
+            for g in pp.gps:
+                if g.get("orf"):
+                    commons.setdefault(g["name"], []).append((a, g))
+        for name, lst in commons.items():
+            for a, ga in lst:
+                va = self.pulsars[a].gp_values(ga, params)
+                for b, gb in lst:
+                    if b == a:
+                        continue
+                    gam = orf_value(ga["orf"], np.asarray(self.pulsars[a].psr.pos, float),
+                                    np.asarray(self.pulsars[b].psr.pos, float))
+                    ia = off[a] + np.asarray(ga["idx"])
+                    ib = off[b] + np.asarray(gb["idx"])
+                    Phi[ia, ib] += gam * va
+        return Phi, off
+
+    @staticmethod
+    def phiinv_cliques(Phi):
+        """[ent] PTA.get_phiinv(method='cliques'): invert each connected
+        block (clique) of Phi by cho_factor; log|Phi| from the same factors."""
+        from scipy.sparse.csgraph import connected_components
+        ncomp, lab = connected_components(Phi != 0, directed=False)
+        inv = np.zeros_like(Phi)
+        logdet = 0.0
+        for c in range(ncomp):
+            ix = np.flatnonzero(lab == c)
+            sub = Phi[np.ix_(ix, ix)]
+            if len(ix) == 1:
+                inv[ix[0], ix[0]] = 1.0 / sub[0, 0]
+                logdet += np.log(sub[0, 0])
+            else:
+                cf = sl.cho_factor(sub)
+                inv[np.ix_(ix, ix)] = sl.cho_solve(cf, np.eye(len(ix)))
+                logdet += 2 * np.sum(np.log(np.diag(cf[0])))
+        return inv, logdet
+
+    def lnlikelihood_correlated(self, params):
+        """[ent] LogLikelihood.__call__ with pta._commonsignals: Sigma =
+        block_diag(TNT_a) + Phi^-1 over all pulsars, one dense Cholesky
+        (enterprise: sksparse cholesky, scipy dense fallback)."""
+        terms = [self.fixed[i] if self.fixed is not None else pp.white_terms(params)
+                 for i, pp in enumerate(self.pulsars)]
+        loglike = -0.5 * sum(t[2] + t[3] for t in terms)
+        Phi, off = self.phi_global(params)
+        try:
+            phiinv, logdet_phi = self.phiinv_cliques(Phi)
+        except sl.LinAlgError:
+            return -np.inf
+        Sigma = phiinv
+        for a, t in enumerate(terms):
+            Sigma[off[a]:off[a + 1], off[a]:off[a + 1]] += t[0]
+        TNr = np.concatenate([t[1] for t in terms])
+        try:
+            cf = sl.cho_factor(Sigma)
+            expval = sl.cho_solve(cf, TNr)
+        except sl.LinAlgError:
+            return -np.inf
+        logdet_sigma = 2 * np.sum(np.log(np.diag(cf[0])))
+        return loglike + 0.5 * (np.dot(TNr, expval) - logdet_sigma - logdet_phi)
+
     def lnlikelihood(self, params):
+        if self.correlated():
+            return self.lnlikelihood_correlated(params)
         loglike = 0.0
         rnr_ld = []
         red = 0.0

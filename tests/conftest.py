@@ -46,6 +46,9 @@ def oracle_lnl_cond(pta, X):
         d = dict(const)
         d.update(pta.map_params(x))
         out.append(o.lnlikelihood(d))
+        if o.correlated():
+            cond.append(correlated_min_eig(o, d))
+            continue
         mins = []
         for i, pp in enumerate(o.pulsars):
             TNT = o.fixed[i][0] if o.fixed is not None else pp.white_terms(d)[0]
@@ -73,7 +76,8 @@ def load_golden(name):
     return pta, z["theta"], z["lnl"], z["min_eig"]
 
 
-GOLDEN_NAMES = ["c1_j1832", "c1_turnover", "c2_small", "c2_chromvary", "c3_small", "c3_freesp", "c4_small"]
+GOLDEN_NAMES = ["c1_j1832", "c1_turnover", "c2_small", "c2_chromvary", "c3_small", "c3_freesp", "c4_small",
+                "c5_small", "c5_mono"]
 
 
 def gpu_available():
@@ -88,3 +92,15 @@ def gpu_available():
 def require_gpu():
     if not gpu_available():
         pytest.fail("this test needs a HIP GPU (run with -m 'not gpu' on CPU-only hosts)")
+
+
+def correlated_min_eig(o, d):
+    """lambda_min of the unit-diagonal-scaled global Sigma = blockdiag(TNT) +
+    Phi^-1 of a correlated PTA (the conditioning of its one factorisation)."""
+    terms = [o.fixed[i] if o.fixed is not None else pp.white_terms(d) for i, pp in enumerate(o.pulsars)]
+    Phi, off = o.phi_global(d)
+    S, _ = o.phiinv_cliques(Phi)
+    for a, t in enumerate(terms):
+        S[off[a]:off[a + 1], off[a]:off[a + 1]] += t[0]
+    sc = 1.0 / np.sqrt(np.abs(np.diag(S)))
+    return np.linalg.eigvalsh(S * sc[:, None] * sc[None, :])[0]

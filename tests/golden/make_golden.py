@@ -38,6 +38,9 @@ def oracle_lnl(pta, X):
         d = dict(const)
         d.update(pta.map_params(x))
         out.append(o.lnlikelihood(d))
+        if o.correlated():
+            cond.append(correlated_min_eig(o, d))
+            continue
         mins = []
         for i, pp in enumerate(o.pulsars):
             TNT = o.fixed[i][0] if fixed is not None else pp.white_terms(d)[0]
@@ -46,6 +49,18 @@ def oracle_lnl(pta, X):
             mins.append(np.linalg.eigvalsh(S * sc[:, None] * sc[None, :])[0])
         cond.append(min(mins))
     return np.array(out), np.array(cond)
+
+
+def correlated_min_eig(o, d):
+    """lambda_min of the unit-diagonal-scaled global Sigma = blockdiag(TNT) +
+    Phi^-1 of a correlated PTA (the conditioning of its one factorisation)."""
+    terms = [o.fixed[i] if o.fixed is not None else pp.white_terms(d) for i, pp in enumerate(o.pulsars)]
+    Phi, off = o.phi_global(d)
+    S, _ = o.phiinv_cliques(Phi)
+    for a, t in enumerate(terms):
+        S[off[a]:off[a + 1], off[a]:off[a + 1]] += t[0]
+    sc = 1.0 / np.sqrt(np.abs(np.diag(S)))
+    return np.linalg.eigvalsh(S * sc[:, None] * sc[None, :])[0]
 
 
 def dump(name, pta, recipe, X):
@@ -82,6 +97,13 @@ def recipe_of(cfg, per_psr, common, fixed_white):
 
 
 def main():
+    only = sys.argv[1:]                    # optional fixture-name prefixes
+    global dump
+    _dump = dump
+
+    def dump(name, *a, **k):               # noqa: F811 - filter by name
+        if not only or any(name.startswith(o) for o in only):
+            _dump(name, *a, **k)
     terms_ecorr = {"efac": "by_backend", "equad": "by_backend", "ecorr": "by_backend",
                    "spin_noise": "powerlaw_30_nfreqs", "dm_noise": "powerlaw_30_nfreqs"}
     # c1: the reference's example pulsar and model (default_noise_example_1.json)
@@ -139,6 +161,12 @@ def main():
     X = np.vstack([synth.prior_draws(pta_c, 8, 17), synth.near_draws(pta_c, truth_c, 8, 18)])
     dump("c2_chromvary", pta_c, {"per_psr_terms": terms_c, "common_terms": {}, "Tspan": float(np.ptp(psr.toas)),
                                  "fixed_white": False, "noisedict": {}}, X)
+    # c5 small: fixed white noise + ECORR, Hellings-Downs correlated common
+    # process (cross-pulsar Sigma), and the same model with a monopole ORF
+    for name, gwb in (("c5_small", "hd_vary_gamma_5_nfreqs"), ("c5_mono", "mono_vary_gamma_4_nfreqs")):
+        c5 = synth.config_c5(n_psr=4, n_toa=500, seed=50, epoch_size=4, gwb=gwb, nfreqs=10)
+        X = np.vstack([synth.prior_draws(c5.pta, 8, 51), synth.near_draws(c5.pta, c5.truth, 8, 52)])
+        dump(name, c5.pta, recipe_of(c5, c5.terms, c5.common, True), X)
 
 
 if __name__ == "__main__":

@@ -180,11 +180,22 @@ def test_extra_model_terms_merge():
     assert out["J1"]["system_noise"] == ["A", "B"] and out["J2"] == {"efac": "by_backend"}
 
 
-def test_hd_is_reported_as_next_row():
-    from enterprise_warp_amd.models import StandardModels
-    c = synth.config_c3(n_psr=2, n_min=600, n_max=700)
-    psrs = [x.psr for x in c.pta.signal_collections]
-    ns = synth.params_namespace(15 * 3.15e7, True)
-    sig = StandardModels(psr=psrs, params=ns).gwb("hd_vary_gamma_14_nfreqs")
-    with pytest.raises(NotImplementedError):
-        sig(psrs[0])
+def test_hd_layout_puts_common_columns_last():
+    """Correlated common process: each pulsar's device layout is [timing
+    model | own columns | common columns in frequency order]; the common
+    signal's phi goes to the PTA-level descriptor with the ORF matrix."""
+    from enterprise_warp_amd.models import hd_orf
+    c5 = synth.config_c5(n_psr=3, n_toa=300, seed=9, epoch_size=4, gwb="hd_vary_gamma_5_nfreqs", nfreqs=10)
+    pta = c5.pta
+    assert pta.correlated()
+    cl = pta.common_layout()
+    assert cl["n_col"] == 10 and cl["kind"] == "hd"
+    pos = [c.psr.pos for c in pta.signal_collections]
+    assert cl["orf"][0, 0] == 1.0 and np.isclose(cl["orf"][0, 1], hd_orf(pos[0], pos[1]))
+    for c, L in zip(pta.signal_collections, pta.layout()):
+        m = L["T"].shape[1]
+        assert L["n_common"] == 10
+        np.testing.assert_array_equal(L["T"][:, m - 10:], c.T[:, c.common["cols"]])
+        np.testing.assert_array_equal(L["T"][:, :L["n_lead"]], c.T[:, :L["n_lead"]])
+        # red noise merged onto the common columns stays in the pulsar's table
+        assert sum(1 for e in L["spec"] if e[1] >= m - 10) == 10

@@ -144,3 +144,37 @@ def test_oracle_fixed_white_equals_varying():
         d.update(pta.map_params(x))
         la, lb = a.lnlikelihood(d), b.lnlikelihood(d)
         assert abs(la - lb) <= 1e-9 * abs(la)
+
+
+@pytest.mark.parametrize("gwb", ["hd_vary_gamma_4_nfreqs", "mono_vary_gamma_3_nfreqs", "dipo_vary_gamma_3_nfreqs",
+                                 "hd_noauto_vary_gamma_3_nfreqs"])
+def test_correlated_woodbury_matches_dense(gwb):
+    """Correlated common process (enterprise_models.py:390-415): the cliques /
+    global-Sigma route == the dense covariance C = N + T Phi T^T with the
+    cross-pulsar ORF blocks (finite timing-model prior)."""
+    from oracle.dense_ref import dense_lnl_pta, woodbury_lnl_pta
+    c = synth.config_c5(n_psr=3, n_toa=150, seed=7, epoch_size=4, gwb=gwb, nfreqs=6)
+    o = oracle_for(c.pta, fixed=False)
+    assert o.correlated()
+    a = dense_lnl_pta(o, c.truth, 1e-12)
+    b = woodbury_lnl_pta(o, c.truth, 1e-12)
+    assert abs(a - b) <= 1e-9 * abs(a)
+
+
+def test_correlated_reduces_to_curn_without_cross_terms():
+    """With the ORF's cross terms removed (Gamma = I) the correlated oracle
+    equals the per-pulsar (CURN) oracle on the same model."""
+    c = synth.config_c5(n_psr=3, n_toa=200, seed=8, epoch_size=4, gwb="hd_vary_gamma_4_nfreqs", nfreqs=6)
+    o = oracle_for(c.pta, fixed=False)
+    import oracle.enterprise_ref as ref
+    saved = ref.orf_value
+    try:
+        ref.orf_value = lambda kind, p1, p2: 1.0 if np.all(p1 == p2) else 0.0
+        corr = o.lnlikelihood(c.truth)
+    finally:
+        ref.orf_value = saved
+    for pp in o.pulsars:
+        for g in pp.gps:
+            g.pop("orf", None)
+    curn = o.lnlikelihood(c.truth)
+    assert abs(corr - curn) <= 1e-10 * abs(curn)
