@@ -215,9 +215,12 @@ __global__ __launch_bounds__(256) void chol_lds_kernel(const CholJob* __restrict
 
 // M_g^-1 and log|M_g| by in-place Gauss-Jordan (SPD: no pivoting needed).
 // grid (n_c, Bc), 256 threads, dynamic LDS (P (P+1) + 3 P) doubles.
+// grid.x runs over the distinct M_g (sin / cos columns of one frequency share
+// it): slot blockIdx.x stands for common column uniq[blockIdx.x].
 __global__ __launch_bounds__(256) void common_minv_kernel(const CommonPsr* __restrict__ cps, int P,
                                                           const double* __restrict__ orf,
                                                           const DSpec* __restrict__ cspec, int nc,
+                                                          const int* __restrict__ uniq,
                                                           const double* __restrict__ theta, int ldth, int b0,
                                                           double* __restrict__ minv, double* __restrict__ mlog) {
   extern __shared__ __attribute__((aligned(16))) double sm[];
@@ -227,7 +230,7 @@ __global__ __launch_bounds__(256) void common_minv_kernel(const CommonPsr* __res
   double* rowk = colk + P;
   double* own = rowk + P;
   __shared__ double red[4];
-  const int g = blockIdx.x, bl = blockIdx.y;
+  const int slot = blockIdx.x, g = uniq[slot], bl = blockIdx.y;
   const double* th = theta + (long long)(b0 + bl) * ldth;
   const double pc = spec_phi(cspec[g], th);
   for (int a = threadIdx.x; a < P; a += 256) {
@@ -264,18 +267,19 @@ __global__ __launch_bounds__(256) void common_minv_kernel(const CommonPsr* __res
     }
     __syncthreads();
   }
-  double* out = minv + ((long long)bl * nc + g) * P * P;
+  double* out = minv + ((long long)bl * nc + slot) * P * P;
   for (int idx = threadIdx.x; idx < P * P; idx += 256) {
     const int i = idx / P, j = idx - i * P;
     out[idx] = M[i * LDP + j];
   }
-  if (threadIdx.x == 0) mlog[(long long)bl * nc + g] = ok ? lsum : __builtin_nan("");
+  if (threadIdx.x == 0) mlog[(long long)bl * nc + slot] = ok ? lsum : __builtin_nan("");
 }
 
 // Dense Sigma_c (Np x Np, row-major) of sample bl, one row per workgroup:
 // rows/cols (a, g) -> a nc + g; r at Np - 1; pad rows/cols identity.
 __global__ __launch_bounds__(256) void common_assemble_kernel(const double* __restrict__ keep, int KD, int P, int nc,
-                                                              const double* __restrict__ minv, int Np,
+                                                              const double* __restrict__ minv,
+                                                              const int* __restrict__ rep, int Np,
                                                               double* __restrict__ mats) {
   const int i = blockIdx.x, bl = blockIdx.y;
   const int N = P * nc;
@@ -285,7 +289,7 @@ __global__ __launch_bounds__(256) void common_assemble_kernel(const double* __re
   if (i < N) {
     const int a = i / nc, g = i - a * nc;
     const double* ka = kb + (long long)a * KD * KD + g * KD;       // row g of pulsar a's kept square
-    const double* mg = mb + (long long)g * P * P + (long long)a * P;  // row a of M_g^-1
+    const double* mg = mb + (long long)rep[g] * P * P + (long long)a * P;  // row a of M_g^-1
     for (int j = threadIdx.x; j < Np; j += 256) {
       double v = 0.0;
       if (j < N) {
@@ -352,20 +356,20 @@ __global__ __launch_bounds__(256) void dchol_diag_kernel(double* __restrict__ ma
     }
     __syncthreads();
   }
-  if (t < DCB) {                              // column t of L^-1
-    for (int i = 0; i < DCB; ++i) {
-      double v;
-      if (i < t) v = 0.0;
-      else if (i == t) v = 1.0 / L[t][t];
-      else {
-        double sacc = 0.0;
-        for (int l = t; l < i; ++l) sacc = fma(L[i][l], Wl[l][t], sacc);
-        v = -sacc / L[i][i];
-      }
-      Wl[i][t] = v;
-    }
-  }
+  // W = L^-1 by forward elimination on [L | I], all threads: step k scales row
+  // k of W by 1/L_kk, then eliminates column k from the rows below
+  for (int idx = t; idx < DCB * DCB; idx += 256) Wl[idx / DCB][idx % DCB] = (idx / DCB == idx % DCB) ? 1.0 : 0.0;
   __syncthreads();
+  for (int k2 = 0; k2 < DCB; ++k2) {
+    const double rk = 1.0 / L[k2][k2];
+    if (t <= k2) Wl[k2][t] *= rk;
+    __syncthreads();
+    for (int idx = t; idx < (DCB - 1 - k2) * (k2 + 1); idx += 256) {
+      const int i = k2 + 1 + idx / (k2 + 1), cc = idx % (k2 + 1);
+      Wl[i][cc] -= L[i][k2] * Wl[k2][cc];
+    }
+    __syncthreads();
+  }
   double* W = wbuf + (long long)bl * DCB * DCB;
   for (int idx = t; idx < DCB * DCB; idx += 256) W[idx] = Wl[idx / DCB][idx % DCB];
   if (t == 0) {
@@ -438,14 +442,68 @@ __global__ __launch_bounds__(256) void dchol_update_kernel(double* __restrict__ 
     for (int r = 0; r < 4; ++r) Aij[(long long)(16 * w + q + 4 * r) * Np + 16 * jb + c] = acc[jb][r];
 }
 
+// Row-oriented (left-looking) update, the default: before block row i is
+// factored, A_ij -= sum_{p < i} U_pi^T U_pj for every j >= i.  One workgroup
+// per (j, sample) keeps its 64 x 64 tile in registers across all p (K = 64 i),
+// staging U_pi / U_pj through LDS with the next pair prefetched into
+// registers: each tile is read and written once per factorisation instead of
+// once per panel step (the right-looking dchol_update_kernel above).
+__global__ __launch_bounds__(256) void dchol_rowupdate_kernel(double* __restrict__ mats, int Np, int i) {
+  __shared__ double Ui[DCB][DCB + 1];
+  __shared__ double Uj[DCB][DCB + 1];
+  const int j = i + blockIdx.x, bl = blockIdx.y, t = threadIdx.x;
+  double* base = mats + (long long)bl * Np * Np;
+  double* Aij = base + (long long)(DCB * i) * Np + DCB * j;
+  const int w = t >> 6, lane = t & 63, q = lane >> 4, c = lane & 15;
+  v4d acc[4];
+#pragma unroll
+  for (int jb = 0; jb < 4; ++jb)
+#pragma unroll
+    for (int r = 0; r < 4; ++r) acc[jb][r] = Aij[(long long)(16 * w + q + 4 * r) * Np + 16 * jb + c];
+  double pf[32];
+  auto gload = [&](int p) {
+    const double* rp = base + (long long)(DCB * p) * Np;
+#pragma unroll
+    for (int r = 0; r < 16; ++r) {
+      const int idx = t + 256 * r, row = idx >> 6, col = idx & 63;
+      pf[r] = rp[(long long)row * Np + DCB * i + col];
+      pf[16 + r] = rp[(long long)row * Np + DCB * j + col];
+    }
+  };
+  gload(0);
+  for (int p = 0; p < i; ++p) {
+    __syncthreads();
+#pragma unroll
+    for (int r = 0; r < 16; ++r) {
+      const int idx = t + 256 * r, row = idx >> 6, col = idx & 63;
+      Ui[row][col] = pf[r];
+      Uj[row][col] = pf[16 + r];
+    }
+    __syncthreads();
+    if (p + 1 < i) gload(p + 1);
+#pragma unroll
+    for (int ts = 0; ts < DCB / 4; ++ts) {
+      const double a = -Ui[4 * ts + q][16 * w + c];
+#pragma unroll
+      for (int jb = 0; jb < 4; ++jb)
+        acc[jb] = __builtin_amdgcn_mfma_f64_16x16x4f64(a, Uj[4 * ts + q][16 * jb + c], acc[jb], 0, 0, 0);
+    }
+  }
+#pragma unroll
+  for (int jb = 0; jb < 4; ++jb)
+#pragma unroll
+    for (int r = 0; r < 4; ++r) Aij[(long long)(16 * w + q + 4 * r) * Np + 16 * jb + c] = acc[jb][r];
+}
+
 // Global term of sample b: units[P * B + b] = -1/2 (log|Sigma_c| + q_c + sum_g log|M_g|).
 __global__ void common_final_kernel(const double* __restrict__ ldet, const double* __restrict__ qv,
-                                    const int* __restrict__ fail, const double* __restrict__ mlog, int nc, int Bc,
-                                    int b0, int P, int B, double* __restrict__ units) {
+                                    const int* __restrict__ fail, const double* __restrict__ mlog,
+                                    const int* __restrict__ rep, int nc, int Bc, int b0, int P, int B,
+                                    double* __restrict__ units) {
   const int bl = blockIdx.x * blockDim.x + threadIdx.x;
   if (bl >= Bc) return;
   double ml = 0.0;
-  for (int g = 0; g < nc; ++g) ml += mlog[(long long)bl * nc + g];
+  for (int g = 0; g < nc; ++g) ml += mlog[(long long)bl * nc + rep[g]];
   double v = -0.5 * (ldet[bl] + qv[bl] + ml);
   if (fail[bl] || !(qv[bl] == qv[bl]) || !(ml == ml)) v = -INFINITY;
   units[(long long)P * B + b0 + bl] = v;
@@ -517,6 +575,9 @@ struct ewh_handle {
   int nc = 0, keep = 0, Np = 0, cchunk = 0;
   double* d_orf = nullptr;
   DSpec* d_cspec = nullptr;
+  int* d_cuniq = nullptr;     // distinct M_g: representative common column per slot
+  int* d_crep = nullptr;      // common column -> slot
+  int nuniq = 0;
   CommonPsr* d_cps = nullptr;
   double *d_keep = nullptr, *d_minv = nullptr, *d_mlog = nullptr, *d_dense = nullptr, *d_wbuf = nullptr;
   double *d_cldet = nullptr, *d_cq = nullptr;
@@ -840,12 +901,49 @@ int setup_common(ewh_handle* h, const ewh_pta_desc* d) {
   std::vector<DSpec> cs(c.n_col);
   for (int g = 0; g < c.n_col; ++g) cs[g] = to_dspec(c.spec[g], g);
   if ((rc = dupload(h, &h->d_cspec, cs.data(), cs.size()))) return rc;
+  // columns whose M_g is identical (the sin / cos pair of a frequency: same
+  // common spectrum, same own spectra in every pulsar) share one inverse
+  auto same_ent = [](const ewh_spec_entry& x, const ewh_spec_entry& y) {
+    auto pr = [](const ewh_pref& a, const ewh_pref& b) { return a.idx == b.idx && a.cval == b.cval; };
+    return x.kind == y.kind && pr(x.p0, y.p0) && pr(x.p1, y.p1) && pr(x.p2, y.p2) && x.f == y.f && x.df == y.df &&
+           x.fyr == y.fyr;
+  };
+  auto own_entries = [&](int p, int g) {
+    const ewh_pulsar_desc& sd = d->pulsars[p];
+    const int col = sd.n_col - sd.n_common + g;
+    std::vector<ewh_spec_entry> v;
+    for (int e = 0; e < sd.n_spec; ++e)
+      if (sd.spec[e].col == col) v.push_back(sd.spec[e]);
+    return v;
+  };
+  std::vector<int> uniq, rep(c.n_col);
+  for (int g = 0; g < c.n_col; ++g) {
+    int found = -1;
+    for (size_t u = 0; u < uniq.size() && found < 0; ++u) {
+      const int g2 = uniq[u];
+      bool eq = same_ent(c.spec[g], c.spec[g2]);
+      for (int p = 0; p < P && eq; ++p) {
+        const auto a = own_entries(p, g), b = own_entries(p, g2);
+        eq = a.size() == b.size();
+        for (size_t k = 0; k < a.size() && eq; ++k) eq = same_ent(a[k], b[k]);
+      }
+      if (eq) found = (int)u;
+    }
+    if (found < 0) {
+      found = (int)uniq.size();
+      uniq.push_back(g);
+    }
+    rep[g] = found;
+  }
+  h->nuniq = (int)uniq.size();
+  if ((rc = dupload(h, &h->d_cuniq, uniq.data(), uniq.size()))) return rc;
+  if ((rc = dupload(h, &h->d_crep, rep.data(), rep.size()))) return rc;
   std::vector<CommonPsr> cps(P);
   for (int p = 0; p < P; ++p) cps[p] = CommonPsr{h->psr[p].d_fx_colptr, h->psr[p].d_fx_spec, h->psr[p].gstart, 0};
   if ((rc = dupload(h, &h->d_cps, cps.data(), cps.size()))) return rc;
   h->Np = DCB * ((P * h->nc + 1 + DCB - 1) / DCB);
   const double per = (double)h->Np * h->Np * 8.0;
-  h->cchunk = (int)std::max(1.0, std::min(1024.0, 12.0e9 / per));
+  h->cchunk = (int)std::max(1.0, std::min(1024.0, 40.0e9 / per));   // <= 40 GB of dense Sigma_c per chunk
   const size_t Bc = h->cchunk;
   if ((rc = dalloc(h, &h->d_minv, Bc * h->nc * P * P))) return rc;
   if ((rc = dalloc(h, &h->d_mlog, Bc * h->nc))) return rc;
@@ -891,24 +989,28 @@ int lnl_correlated(ewh_handle* h, const double* theta_dev, int B, hipStream_t st
   const size_t lds = ((size_t)P * (P + 1) + 3 * P) * sizeof(double);
   for (int c0 = 0; c0 < B; c0 += h->cchunk) {
     const int nb = std::min(h->cchunk, B - c0);
-    hipLaunchKernelGGL(common_minv_kernel, dim3(h->nc, nb), dim3(256), lds, st, h->d_cps, P, h->d_orf, h->d_cspec,
-                       h->nc, theta_dev, ldth, c0, h->d_minv, h->d_mlog);
+    hipLaunchKernelGGL(common_minv_kernel, dim3(h->nuniq, nb), dim3(256), lds, st, h->d_cps, P, h->d_orf,
+                       h->d_cspec, h->nc, h->d_cuniq, theta_dev, ldth, c0, h->d_minv, h->d_mlog);
     hipLaunchKernelGGL(common_assemble_kernel, dim3(h->Np, nb), dim3(256), 0, st,
-                       h->d_keep + (size_t)c0 * P * KD * KD, KD, P, h->nc, h->d_minv, h->Np, h->d_dense);
+                       h->d_keep + (size_t)c0 * P * KD * KD, KD, P, h->nc, h->d_minv, h->d_crep, h->Np,
+                       h->d_dense);
     EWH_HIP(hipMemsetAsync(h->d_cldet, 0, sizeof(double) * nb, st));
     EWH_HIP(hipMemsetAsync(h->d_cq, 0, sizeof(double) * nb, st));
     EWH_HIP(hipMemsetAsync(h->d_cfail, 0, sizeof(int) * nb, st));
     for (int k = 0; k < nbk; ++k) {
+      const int m = nbk - k - 1;
+      if (h->kernel_mode != 7 && k > 0)     // row-oriented update of block row k (default)
+        hipLaunchKernelGGL(dchol_rowupdate_kernel, dim3(m + 1, nb), dim3(256), 0, st, h->d_dense, h->Np, k);
       hipLaunchKernelGGL(dchol_diag_kernel, dim3(nb), dim3(256), 0, st, h->d_dense, h->Np, k, h->d_wbuf, h->d_cldet,
                          h->d_cq, h->d_cfail);
-      const int m = nbk - k - 1;
       if (m > 0) {
         hipLaunchKernelGGL(dchol_panel_kernel, dim3(m, nb), dim3(256), 0, st, h->d_dense, h->Np, k, h->d_wbuf);
-        hipLaunchKernelGGL(dchol_update_kernel, dim3(m * (m + 1) / 2, nb), dim3(256), 0, st, h->d_dense, h->Np, k);
+        if (h->kernel_mode == 7)            // A/B: right-looking trailing update
+          hipLaunchKernelGGL(dchol_update_kernel, dim3(m * (m + 1) / 2, nb), dim3(256), 0, st, h->d_dense, h->Np, k);
       }
     }
     hipLaunchKernelGGL(common_final_kernel, dim3((nb + 255) / 256), dim3(256), 0, st, h->d_cldet, h->d_cq,
-                       h->d_cfail, h->d_mlog, h->nc, nb, c0, P, B, h->d_units);
+                       h->d_cfail, h->d_mlog, h->d_crep, h->nc, nb, c0, P, B, h->d_units);
     EWH_HIP(hipGetLastError());
   }
   return 0;

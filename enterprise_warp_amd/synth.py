@@ -316,7 +316,7 @@ def config_c5(n_psr=100, n_toa=20000, seed=100, epoch_size=16, gwb="hd_vary_gamm
     pta = build_pta(psrs, terms, {"gwb": gwb}, ns, wn)
     truth = truth_values(pta, seed + 2, white=wn)
     simulate_residuals(pta, truth, seed + 3)
-    return SimpleNamespace(name="C5", pta=pta, truth=truth, B=256, theta_seed=seed, terms=terms,
+    return SimpleNamespace(name="C5", pta=pta, truth=truth, B=512, theta_seed=seed, terms=terms,
                            common={"gwb": gwb})
 
 
