@@ -524,6 +524,14 @@ __device__ __forceinline__ void syrk_update(v4d& C, const v4d& Ui, const v4d& Uj
 // pivots are factored by VALU (ALG 1: row k broadcast by ds_bpermute, ALG 2:
 // through the per-wave LDS `rowbuf`), then the block row is scaled to
 // U = D^-1/2 V.  Accumulates log d_k (one lane per row) and d_k > 0 per lane.
+// lane (q, c) <- lane (q, K) of its 16-lane row (DPP row_newbcast, gfx90a+)
+template <int K>
+__device__ __forceinline__ double row_newbcast(double x) {
+  const int lo = __builtin_amdgcn_update_dpp(0, __double2loint(x), 0x150 + K, 0xf, 0xf, false);
+  const int hi = __builtin_amdgcn_update_dpp(0, __double2hiint(x), 0x150 + K, 0xf, 0xf, false);
+  return __hiloint2double(hi, lo);
+}
+
 template <int NB, int FULL, int ALG, typename BBt, typename Blk>
 __device__ __forceinline__ void panel_ldl_row(BBt BBc, Blk&& blk, int q, int c, LogAcc& ldet, bool& ok,
                                               double* rowbuf) {
@@ -531,8 +539,37 @@ __device__ __forceinline__ void panel_ldl_row(BBt BBc, Blk&& blk, int q, int c, 
   (void)rowbuf;
   (void)LD;
   constexpr int bb = decltype(BBc)::value;
+  static_assert(ALG != 3 || FULL, "the DPP panel needs compile-time pivots");
   static_for<0, 4>([&](auto KR) {
     constexpr int kr = decltype(KR)::value;
+    // ALG 3: u_i = A[q + 4r][k] read from the SYMMETRIC lower part of the
+    // diagonal block (lane (q, k), register r: kept exact by the full-block
+    // updates) with one DPP row broadcast per register -- no ds_bpermute
+    auto step3 = [&](auto KQc) {
+      constexpr int kq = decltype(KQc)::value;
+      constexpr int k = 4 * kr + kq;
+      const double d = readlane_d(blk(BBc)[kr], 16 * kq + k);
+      double ui[4];
+      double rk[NB];
+      static_for<kr, 4>([&](auto R) {
+        constexpr int r = decltype(R)::value;
+        const double v = row_newbcast<k>(blk(BBc)[r]);
+        ui[r] = (r > kr || q > kq) ? v : 0.0;
+      });
+      static_for<bb, NB>([&](auto JJ) {
+        constexpr int j = decltype(JJ)::value;
+        rk[j] = __shfl(blk(JJ)[kr], 16 * kq + c);
+      });
+      const double dinv = rcp_nr(d);
+      static_for<kr, 4>([&](auto R) { ui[decltype(R)::value] *= dinv; });
+      static_for<bb, NB>([&](auto JJ) {
+        constexpr int j = decltype(JJ)::value;
+        static_for<kr, 4>([&](auto R) {
+          constexpr int r = decltype(R)::value;
+          blk(JJ)[r] = fma(-ui[r], rk[j], blk(JJ)[r]);
+        });
+      });
+    };
     auto step = [&](const int kq) {
       const int k = 4 * kr + kq;
       const double d = readlane_d(blk(BBc)[kr], 16 * kq + k);            // wave-uniform pivot
@@ -588,7 +625,9 @@ __device__ __forceinline__ void panel_ldl_row(BBt BBc, Blk&& blk, int q, int c, 
       });
     };
     constexpr int nk = (bb == NB - 1 && kr == 3) ? 3 : 4;   // the r column is not pivoted
-    if constexpr (FULL) {
+    if constexpr (ALG == 3) {
+      static_for<0, nk>([&](auto KQ) { step3(KQ); });
+    } else if constexpr (FULL) {
       static_for<0, nk>([&](auto KQ) {
         step(decltype(KQ)::value);
         // unrolled LDS-broadcast steps: keep the scheduler from hoisting the

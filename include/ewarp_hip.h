@@ -176,7 +176,7 @@ double ewh_unit_cost(const ewh_handle* h, int32_t pulsar);
  * LDL^T panel when the reduced matrix fits, LDS kernel otherwise), 1 = force
  * the LDS kernel, 2 = the round-1 MFMA kernel (Cholesky panel, looped steps).
  * A/B variants for NB = 8 only (else as 0): 3 = LDL^T at one wave per SIMD,
- * 4 = LDL^T with looped steps, 5 = Cholesky panel with unrolled steps,
+ * 4 = LDL^T with looped steps, 5 = LDL^T with u_i by ds_bpermute (unrolled),
  * 6 = LDL^T with the row broadcast through LDS.  7 = default Cholesky with
  * the round-1 contraction (varying white noise: separate epoch-sum kernel,
  * unpipelined tiles) instead of the pipelined one. */
