@@ -19,7 +19,7 @@ int launch_chol_small(int mode, int nb, const CholJob* jobs, int B, long long u0
   // A/B variants (NB = 8, the C3 reduced width)
   if (nb == 8 && mode >= 3) {
     switch (mode) {
-      case 3: launch_chol_mfma<8, 1, 1, 1>(jobs, B, u0, n, b_off, theta, ldth, units, st); return 0;  // 1 wave/SIMD
+      case 3: launch_chol_mfma<8, 1, 1, 3>(jobs, B, u0, n, b_off, theta, ldth, units, st); return 0;  // 1 wave/SIMD
       case 4: launch_chol_mfma<8, 0, 2, 1>(jobs, B, u0, n, b_off, theta, ldth, units, st); return 0;  // LDL, looped
       case 5: launch_chol_mfma<8, 1, 2, 1>(jobs, B, u0, n, b_off, theta, ldth, units, st); return 0;  // LDL, bpermute u_i
       case 6: launch_chol_mfma<8, 0, 2, 2>(jobs, B, u0, n, b_off, theta, ldth, units, st); return 0;  // LDL, LDS bcast
