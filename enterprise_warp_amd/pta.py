@@ -109,6 +109,17 @@ class PTA:
         d = params if isinstance(params, dict) else self.map_params(params)
         return float(sum(p.get_logpdf(d[p.name]) for p in self._params))
 
+    def get_lnprior_batch(self, X):
+        """log-prior of every row of X [B, nparam] (param_names order)."""
+        X = np.atleast_2d(np.asarray(X, dtype=float))
+        lp = np.zeros(len(X))
+        for p in self._params:
+            i = self._index[p.name]
+            v = X[:, i:i + p.size] if p.size else X[:, i]
+            q = np.asarray(p._logpdf(v), dtype=float)
+            lp += q.sum(axis=1) if q.ndim == 2 else q
+        return lp
+
     def _theta(self, X):
         """dict / ndarray / batch -> theta matrix [B, nparam] (param_names order)."""
         if isinstance(X, dict):

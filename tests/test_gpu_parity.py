@@ -116,3 +116,20 @@ def test_c5_reduced_vs_oracle(require_gpu):
     got = c5.pta.get_lnlikelihood_batch(X)
     want, cond = oracle_lnl_cond(c5.pta, X)
     _check(got, want, cond, "c5_reduced")
+
+
+def test_paramfile_driver_hypermodel(require_gpu, tmp_path, monkeypatch):
+    """examples/run_example_paramfile.py flow on the reference's
+    default_hypermodel.dat (two {N} model blocks -> HyperModel) through
+    enterprise_warp_amd.run: batched device likelihood inside the sampler."""
+    import shutil
+    from conftest import REF_EXAMPLES
+    from enterprise_warp_amd import run
+    for d in ("data", "example_params", "example_noisemodels", "example_noisefiles"):
+        shutil.copytree(f"{REF_EXAMPLES}/{d}", tmp_path / d)
+    monkeypatch.chdir(tmp_path)
+    X, post, like = run.main(["--prfile", "example_params/default_hypermodel.dat", "--niter", "30",
+                              "--nchains", "32", "--seed", "1"])
+    assert X.shape[0] == 32 and np.all(np.isfinite(post))
+    out = list(tmp_path.glob("out/**/chain_1.txt"))
+    assert len(out) == 1 and np.loadtxt(out[0]).shape[0] == 32 * 3

@@ -199,3 +199,59 @@ def test_hd_layout_puts_common_columns_last():
         np.testing.assert_array_equal(L["T"][:, :L["n_lead"]], c.T[:, :L["n_lead"]])
         # red noise merged onto the common columns stays in the pulsar's table
         assert sum(1 for e in L["spec"] if e[1] >= m - 10) == 10
+
+
+class _MockPTA:
+    """Minimal PTA surface (params, param_names, batch lnL / lnprior) with an
+    analytic Gaussian likelihood, for the host-side HyperModel / sampler."""
+
+    def __init__(self, names, mu, sig=0.5):
+        from enterprise_warp_amd import parameter
+        self.params = [parameter.Uniform(-10, 10)(n) for n in names]
+        self.param_names = list(names)
+        self.mu, self.sig = np.asarray(mu, float), sig
+
+    def get_lnlikelihood_batch(self, X):
+        X = np.atleast_2d(X)
+        return -0.5 * np.sum((X - self.mu) ** 2, axis=1) / self.sig ** 2
+
+    def get_lnlikelihood(self, x):
+        return float(self.get_lnlikelihood_batch(np.asarray(x))[0])
+
+    def get_lnprior_batch(self, X):
+        X = np.atleast_2d(X)
+        return np.where(np.all(np.abs(X) <= 10, axis=1), -len(self.param_names) * np.log(20.0), -np.inf)
+
+    def get_lnprior(self, x):
+        return float(self.get_lnprior_batch(np.asarray(x))[0])
+
+
+def test_hypermodel_routes_by_nmodel():
+    """enterprise_extensions HyperModel semantics (run_example_paramfile.py:31-45):
+    union of parameter names in first-appearance order + nmodel; only the
+    active model's likelihood; batch == single calls."""
+    from enterprise_warp_amd.hypermodel import HyperModel
+    a = _MockPTA(["a", "shared"], [1.0, 2.0])
+    b = _MockPTA(["shared", "b"], [3.0, -1.0])
+    hm = HyperModel([a, b])
+    assert hm.param_names == ["a", "shared", "b", "nmodel"]
+    X = np.array([[1.0, 2.0, 0.0, 0.2], [0.0, 3.0, -1.0, 0.9], [0.0, 3.0, -1.0, 1.4], [0, 0, 0, 2.0]])
+    got = hm.get_lnlikelihood_batch(X)
+    assert got[0] == a.get_lnlikelihood([1.0, 2.0]) and got[1] == b.get_lnlikelihood([3.0, -1.0])
+    assert got[2] == got[1] and got[3] == -np.inf
+    np.testing.assert_array_equal([hm.get_lnlikelihood(x) for x in X[:3]], got[:3])
+    lp = hm.get_lnprior_batch(X)
+    assert np.isfinite(lp[:3]).all() and lp[3] == -np.inf
+    assert lp[0] == hm.get_lnprior(X[0])
+
+
+def test_batched_sampler_recovers_gaussian(tmp_path):
+    from enterprise_warp_amd.sampler import BatchedMH
+    m = _MockPTA(["x", "y"], [1.5, -2.0], sig=0.3)
+    s = BatchedMH(m, nchains=64, outdir=str(tmp_path), seed=3, adapt_every=50)
+    X, post, like = s.sample(niter=400, thin=50)
+    H = np.concatenate(s.history[200:])
+    np.testing.assert_allclose(H.mean(axis=0), [1.5, -2.0], atol=0.05)
+    np.testing.assert_allclose(H.std(axis=0), [0.3, 0.3], rtol=0.15)
+    rows = np.loadtxt(tmp_path / "chain_1.txt")
+    assert rows.shape == (64 * 8, 2 + 4)
