@@ -10,7 +10,8 @@ import os
 _HERE = os.path.dirname(os.path.abspath(__file__))
 LIB_PATH = os.path.join(_HERE, "libewarp_hip.so")
 
-EWH_ABI_VERSION = 3
+EWH_ABI_VERSION = 4
+COMMON_CORRELATED, COMMON_OPTSTAT = 0, 1
 SPEC_POWERLAW, SPEC_TURNOVER, SPEC_FREESPEC, SPEC_CONST = 1, 2, 3, 4
 
 
@@ -39,7 +40,7 @@ class PulsarDesc(C.Structure):
 
 
 class CommonDesc(C.Structure):
-    _fields_ = [("n_col", C.c_int32), ("orf", _dp), ("spec", C.POINTER(SpecEntry))]
+    _fields_ = [("n_col", C.c_int32), ("orf", _dp), ("spec", C.POINTER(SpecEntry)), ("kind", C.c_int32)]
 
 
 class PtaDesc(C.Structure):
@@ -48,7 +49,7 @@ class PtaDesc(C.Structure):
 
 
 EXPORTS = ["ewh_create", "ewh_lnl_batch", "ewh_lnl_units_device", "ewh_last_unit_terms", "ewh_unit_cost",
-           "ewh_set_kernel_mode", "ewh_destroy", "ewh_last_error", "ewh_version"]
+           "ewh_set_kernel_mode", "ewh_optstat", "ewh_destroy", "ewh_last_error", "ewh_version"]
 
 _lib = None
 
@@ -87,6 +88,8 @@ def load():
     lib.ewh_unit_cost.restype = C.c_double
     lib.ewh_set_kernel_mode.argtypes = [C.c_void_p, C.c_int32]
     lib.ewh_set_kernel_mode.restype = C.c_int
+    lib.ewh_optstat.argtypes = [C.c_void_p, _dp, C.c_int32, _dp, _dp, _dp, _dp, _dp]
+    lib.ewh_optstat.restype = C.c_int
     lib.ewh_destroy.argtypes = [C.c_void_p]
     lib.ewh_destroy.restype = None
     lib.ewh_last_error.argtypes = []

@@ -681,7 +681,7 @@ void chol_mfma_kernel(const CholJob* __restrict__ jobs, int B, long long u0, int
   LogAcc lphi;
   for (int a = lane; a < LD; a += 64) {
     double pi = 0.0;
-    if (a < J.mreal) {
+    if (a < J.mreal && J.col_ptr[a] < J.col_ptr[a + 1]) {   // (pads carry no entry)
       double ph = 0.0;
       for (int e = J.col_ptr[a]; e < J.col_ptr[a + 1]; ++e) ph += spec_phi_body(J.spec[e], th);
       pi = 1.0 / ph;
@@ -876,7 +876,7 @@ void chol_big_kernel(const CholJob* __restrict__ jobs, int B, long long u0, int 
   LogAcc lphi;
   for (int a = lane; a < LD; a += 64) {
     double pi = 0.0;
-    if (a < J.mreal) {
+    if (a < J.mreal && J.col_ptr[a] < J.col_ptr[a + 1]) {   // (pads carry no entry)
       double ph = 0.0;
       for (int e = J.col_ptr[a]; e < J.col_ptr[a + 1]; ++e) ph += spec_phi_body(J.spec[e], th);
       pi = 1.0 / ph;

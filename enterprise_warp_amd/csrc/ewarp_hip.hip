@@ -495,6 +495,107 @@ __global__ __launch_bounds__(256) void dchol_rowupdate_kernel(double* __restrict
     for (int r = 0; r < 4; ++r) Aij[(long long)(16 * w + q + 4 * r) * Np + 16 * jb + c] = acc[jb][r];
 }
 
+// ----------------------------------------------------------------------------
+// optimal statistic (EWH_COMMON_OPTSTAT handles; ewh_optstat)
+// From pulsar a's kept block K (its common columns G after eliminating the
+// rest, phi^-1 on every column): (Sigma^-1)_GG = K_GG^-1 and
+// (Sigma^-1 d)_G = K_GG^-1 K_Gr, so with D = diag(phi^-1)_G
+//   X = D K_GG^-1 K_Gr,  Z = D - D K_GG^-1 D
+// (F^T P^-1 r and F^T P^-1 F by Woodbury: TNT = Sigma - Phi^-1).  Stored
+// pre-scaled by phihat^1/2: x^ = phihat^1/2 X, W = phihat^1/2 Z phihat^1/2, so
+// that per pair top = x^_a . x^_b and bot = tr(Z_a phihat Z_b phihat) = <W_a, W_b>.
+// ----------------------------------------------------------------------------
+__global__ __launch_bounds__(64) void os_xz_kernel(const double* __restrict__ keep, int KD, int P, int nc,
+                                                   const CommonPsr* __restrict__ cps,
+                                                   const double* __restrict__ theta, int ldth,
+                                                   const double* __restrict__ phihat, double* __restrict__ xh,
+                                                   double* __restrict__ wh) {
+  __shared__ double M[32][33];
+  __shared__ double colk[32], rowk[32], dv[32], kr[32], sq[32];
+  const int a = blockIdx.x, bl = blockIdx.y, t = threadIdx.x;
+  const double* K = keep + ((long long)bl * P + a) * KD * KD;
+  const double* th = theta + (long long)bl * ldth;
+  for (int idx = t; idx < nc * nc; idx += 64) M[idx / nc][idx % nc] = K[(idx / nc) * KD + idx % nc];
+  if (t < nc) {
+    kr[t] = K[t * KD + KD - 1];
+    const CommonPsr c = cps[a];
+    double ph = 0.0;
+    for (int e = c.colptr[c.gstart + t]; e < c.colptr[c.gstart + t + 1]; ++e) ph += spec_phi(c.spec[e], th);
+    dv[t] = 1.0 / ph;
+    sq[t] = sqrt(phihat[(long long)bl * nc + t]);
+  }
+  __syncthreads();
+  for (int k = 0; k < nc; ++k) {        // Gauss-Jordan inverse of K_GG (SPD)
+    const double pinv = 1.0 / M[k][k];
+    if (t < nc) {
+      colk[t] = M[t][k];
+      rowk[t] = M[k][t] * pinv;
+    }
+    __syncthreads();
+    for (int idx = t; idx < nc * nc; idx += 64) {
+      const int i = idx / nc, j = idx % nc;
+      double v;
+      if (i == k) v = (j == k) ? pinv : rowk[j];
+      else if (j == k) v = -colk[i] * pinv;
+      else v = M[i][j] - colk[i] * rowk[j];
+      M[i][j] = v;
+    }
+    __syncthreads();
+  }
+  double* xo = xh + ((long long)bl * P + a) * nc;
+  double* wo = wh + ((long long)bl * P + a) * nc * nc;
+  if (t < nc) {
+    double v = 0.0;
+    for (int h = 0; h < nc; ++h) v += M[t][h] * kr[h];
+    xo[t] = sq[t] * dv[t] * v;
+  }
+  for (int idx = t; idx < nc * nc; idx += 64) {
+    const int g = idx / nc, h = idx % nc;
+    const double z = (g == h ? dv[g] : 0.0) - dv[g] * M[g][h] * dv[h];
+    wo[idx] = sq[g] * z * sq[h];
+  }
+}
+
+// rho_ab, sig_ab for b > a: one wave per pair (lanes over the nc^2 entries).
+__global__ __launch_bounds__(256) void os_pairs_kernel(const double* __restrict__ xh, const double* __restrict__ wh,
+                                                       int P, int nc, double* __restrict__ rho,
+                                                       double* __restrict__ sig) {
+  const int a = blockIdx.x, bl = blockIdx.y, w = threadIdx.x >> 6, lane = threadIdx.x & 63;
+  const double* xa = xh + ((long long)bl * P + a) * nc;
+  const double* wa = wh + ((long long)bl * P + a) * nc * nc;
+  for (int b = a + 1 + w; b < P; b += 4) {
+    const double* xb = xh + ((long long)bl * P + b) * nc;
+    const double* wb = wh + ((long long)bl * P + b) * nc * nc;
+    double top = 0.0, bot = 0.0;
+    for (int g = lane; g < nc; g += 64) top += xa[g] * xb[g];
+    for (int idx = lane; idx < nc * nc; idx += 64) bot += wa[idx] * wb[idx];
+    top = wave_sum(top);
+    bot = wave_sum(bot);
+    if (lane == 0) {
+      rho[((long long)bl * P + a) * P + b] = top / bot;
+      sig[((long long)bl * P + a) * P + b] = 1.0 / sqrt(bot);
+    }
+  }
+}
+
+// OS = sum rho Gamma / sig^2 / sum Gamma^2 / sig^2 per draw (pairs in order).
+__global__ void os_final_kernel(const double* __restrict__ rho, const double* __restrict__ sig,
+                                const double* __restrict__ orf, int P, int B, double* __restrict__ os,
+                                double* __restrict__ os_sig) {
+  const int bl = blockIdx.x * blockDim.x + threadIdx.x;
+  if (bl >= B) return;
+  double num = 0.0, den = 0.0;
+  for (int a = 0; a < P; ++a)
+    for (int b = a + 1; b < P; ++b) {
+      const double s = sig[((long long)bl * P + a) * P + b], r = rho[((long long)bl * P + a) * P + b];
+      const double g = orf[a * P + b];
+      num += r * g / (s * s);
+      den += g * g / (s * s);
+    }
+  os[bl] = num / den;
+  os_sig[bl] = 1.0 / sqrt(den);
+}
+
 // Global term of sample b: units[P * B + b] = -1/2 (log|Sigma_c| + q_c + sum_g log|M_g|).
 __global__ void common_final_kernel(const double* __restrict__ ldet, const double* __restrict__ qv,
                                     const int* __restrict__ fail, const double* __restrict__ mlog,
@@ -583,6 +684,7 @@ struct ewh_handle {
   double *d_cldet = nullptr, *d_cq = nullptr;
   int* d_cfail = nullptr;
   size_t keep_cap = 0;
+  bool osmode = false;        // EWH_COMMON_OPTSTAT handle (ewh_optstat only)
 };
 
 namespace {
@@ -668,10 +770,12 @@ int validate(const ewh_pta_desc* d) {
   }
   if (d->common) {
     const ewh_common_desc& c = *d->common;
-    if (c.n_col < 1 || c.n_col > 31 || !c.orf || !c.spec)
+    if (c.kind != EWH_COMMON_CORRELATED && c.kind != EWH_COMMON_OPTSTAT)
+      return set_err(EWH_E_INVALID, "common: bad kind");
+    if (c.n_col < 1 || c.n_col > 31 || !c.orf || (c.kind == EWH_COMMON_CORRELATED && !c.spec))
       return set_err(EWH_E_INVALID, "common: need 1..31 columns, an ORF matrix and spectral entries");
     if (d->n_pulsar > 128) return set_err(EWH_E_UNSUPPORTED, "common: at most 128 pulsars");
-    for (int g = 0; g < c.n_col; ++g) {
+    for (int g = 0; c.kind == EWH_COMMON_CORRELATED && g < c.n_col; ++g) {
       const ewh_spec_entry& sp = c.spec[g];
       if (sp.col != g || sp.kind < EWH_SPEC_POWERLAW || sp.kind > EWH_SPEC_CONST || sp.p0.idx >= d->n_param ||
           sp.p1.idx >= d->n_param || sp.p2.idx >= d->n_param)
@@ -879,7 +983,11 @@ int setup_fixed(ewh_handle* h, const ewh_pta_desc* d) {
     EWH_HIP(hipStreamSynchronize(h->stream));
     int fail = 0;
     EWH_HIP(hipMemcpy(&fail, h->d_fxfail + p, sizeof(int), hipMemcpyDeviceToHost));
-    jobs[p] = CholJob{ps.d_S, 0, ps.fx_ld, ps.nloc, ps.d_fx_colptr, ps.d_fx_spec, h->d_fxK + p, 0, fail};
+    // mreal: columns that take phi^-1 in the factorisation -- the own columns
+    // (correlated: the common block is assembled globally), or every column
+    // with entries (optimal statistic: the CURN Sigma of each pulsar)
+    const int mreal = h->osmode ? ps.fx_ld - 1 : ps.nloc;
+    jobs[p] = CholJob{ps.d_S, 0, ps.fx_ld, mreal, ps.d_fx_colptr, ps.d_fx_spec, h->d_fxK + p, 0, fail};
   }
   EWH_HIP(hipMemcpy(h->d_jobs_fixed, jobs.data(), sizeof(CholJob) * h->P, hipMemcpyHostToDevice));
   return 0;
@@ -898,6 +1006,12 @@ int setup_common(ewh_handle* h, const ewh_pta_desc* d) {
   }
   int rc;
   if ((rc = dupload(h, &h->d_orf, c.orf, (size_t)P * P))) return rc;
+  if (h->osmode) {               // optimal statistic: the CURN likelihood layout + the ORF only
+    h->corr = false;
+    std::vector<CommonPsr> cps(P);
+    for (int p = 0; p < P; ++p) cps[p] = CommonPsr{h->psr[p].d_fx_colptr, h->psr[p].d_fx_spec, h->psr[p].gstart, 0};
+    return dupload(h, &h->d_cps, cps.data(), cps.size());
+  }
   std::vector<DSpec> cs(c.n_col);
   for (int g = 0; g < c.n_col; ++g) cs[g] = to_dspec(c.spec[g], g);
   if ((rc = dupload(h, &h->d_cspec, cs.data(), cs.size()))) return rc;
@@ -1113,6 +1227,7 @@ int ewh_create(const ewh_pta_desc* d, int device, ewh_handle** out) {
   h->white_fixed = (d->white_fixed != 0) && !any_theta_white;
   if ((rc = dalloc(h, &h->d_jobs_fixed, h->P))) return bail(rc);
   if ((rc = dalloc(h, &h->d_jobs_var, h->P))) return bail(rc);
+  h->osmode = d->common && d->common->kind == EWH_COMMON_OPTSTAT;
   if (d->common && !h->white_fixed)
     return bail(set_err(EWH_E_UNSUPPORTED, "correlated common process: white noise must be fixed (TNT cached)"));
   if (h->white_fixed) {
@@ -1139,6 +1254,7 @@ double ewh_unit_cost(const ewh_handle* h, int32_t p) {
 int ewh_lnl_units_device(ewh_handle* h, const double* theta_dev, int32_t B, int64_t u_begin, int64_t u_end,
                          double* out_dev, void* stream) {
   if (!h || !theta_dev || !out_dev || B <= 0) return set_err(EWH_E_INVALID, "bad arguments");
+  if (h->osmode) return set_err(EWH_E_UNSUPPORTED, "an optimal-statistic handle evaluates ewh_optstat only");
   const long long U = (long long)h->P * B;
   u_begin = std::max<int64_t>(0, u_begin);
   u_end = std::min<int64_t>(U, u_end);
@@ -1236,6 +1352,88 @@ int ewh_lnl_batch(ewh_handle* h, const double* theta_host, int32_t B, double* ou
   if (rc) return rc;
   EWH_HIP(hipMemcpyAsync(out_host, h->d_out, sizeof(double) * B, hipMemcpyDeviceToHost, h->stream));
   EWH_HIP(hipStreamSynchronize(h->stream));
+  return 0;
+}
+
+int ewh_optstat(ewh_handle* h, const double* theta_host, int32_t B, const double* phihat_host, double* rho_host,
+                double* sig_host, double* os_host, double* os_sig_host) {
+  if (!h || !theta_host || !phihat_host || !os_host || !os_sig_host || B <= 0)
+    return set_err(EWH_E_INVALID, "bad arguments");
+  if (!h->osmode) return set_err(EWH_E_INVALID, "handle was not created with common->kind = EWH_COMMON_OPTSTAT");
+  EWH_HIP(hipSetDevice(h->device));
+  const int P = h->P, nc = h->nc, KD = 16 * h->keep, np = std::max(1, h->n_param);
+  hipStream_t st = h->stream;
+  int rc;
+  double *th, *ph, *xh, *wh, *rho, *sig, *os;
+  std::vector<void*> tmp;
+  auto alloc = [&](double** p, size_t n) {
+    int r = dalloc(h, p, n);
+    if (!r) tmp.push_back(*p);
+    return r;
+  };
+  auto release = [&]() {
+    for (void* p : tmp) {
+      (void)hipFree(p);
+      h->allocs.erase(std::find(h->allocs.begin(), h->allocs.end(), p));
+    }
+  };
+  if ((rc = alloc(&th, (size_t)B * np)) || (rc = alloc(&ph, (size_t)B * nc)) ||
+      (rc = alloc(&xh, (size_t)B * P * nc)) || (rc = alloc(&wh, (size_t)B * P * nc * nc)) ||
+      (rc = alloc(&rho, (size_t)B * P * P)) || (rc = alloc(&sig, (size_t)B * P * P)) || (rc = alloc(&os, 2 * (size_t)B))) {
+    release();
+    return rc;
+  }
+  if (h->n_param > 0)
+    EWH_HIP(hipMemcpyAsync(th, theta_host, sizeof(double) * (size_t)B * h->n_param, hipMemcpyHostToDevice, st));
+  EWH_HIP(hipMemcpyAsync(ph, phihat_host, sizeof(double) * (size_t)B * nc, hipMemcpyHostToDevice, st));
+  EWH_HIP(hipMemsetAsync(rho, 0, sizeof(double) * (size_t)B * P * P, st));
+  EWH_HIP(hipMemsetAsync(sig, 0, sizeof(double) * (size_t)B * P * P, st));
+  if ((rc = ensure_units(h, B))) {
+    release();
+    return rc;
+  }
+  const size_t need = (size_t)B * P * KD * KD;
+  if (need > h->keep_cap) {
+    if (h->d_keep) {
+      (void)hipFree(h->d_keep);
+      h->allocs.erase(std::find(h->allocs.begin(), h->allocs.end(), (void*)h->d_keep));
+      h->d_keep = nullptr;
+    }
+    h->keep_cap = 0;
+    if ((rc = dalloc(h, &h->d_keep, need))) {
+      release();
+      return rc;
+    }
+    h->keep_cap = need;
+  }
+  const long long U = (long long)P * B;
+  for (long long u = 0; u < U;) {      // per-pulsar factorisations, common block kept
+    const int p0 = (int)(u / B);
+    const int nb0 = h->psr[p0].fx_nb;
+    int p1 = p0 + 1;
+    while (p1 < P && h->psr[p1].fx_nb == nb0) ++p1;
+    const long long seg_end = (long long)p1 * B;
+    if ((rc = launch_partial_nb(nb0, h->keep, h->d_jobs_fixed, B, u, seg_end - u, th, h->n_param, h->d_units,
+                                h->d_keep, P, st))) {
+      release();
+      return rc;
+    }
+    u = seg_end;
+  }
+  hipLaunchKernelGGL(os_xz_kernel, dim3(P, B), dim3(64), 0, st, h->d_keep, KD, P, nc, h->d_cps, th, h->n_param, ph,
+                     xh, wh);
+  hipLaunchKernelGGL(os_pairs_kernel, dim3(P, B), dim3(256), 0, st, xh, wh, P, nc, rho, sig);
+  hipLaunchKernelGGL(os_final_kernel, dim3((B + 255) / 256), dim3(256), 0, st, rho, sig, h->d_orf, P, B, os, os + B);
+  hipError_t e = hipGetLastError();
+  if (e == hipSuccess && rho_host)
+    e = hipMemcpyAsync(rho_host, rho, sizeof(double) * (size_t)B * P * P, hipMemcpyDeviceToHost, st);
+  if (e == hipSuccess && sig_host)
+    e = hipMemcpyAsync(sig_host, sig, sizeof(double) * (size_t)B * P * P, hipMemcpyDeviceToHost, st);
+  if (e == hipSuccess) e = hipMemcpyAsync(os_host, os, sizeof(double) * B, hipMemcpyDeviceToHost, st);
+  if (e == hipSuccess) e = hipMemcpyAsync(os_sig_host, os + B, sizeof(double) * B, hipMemcpyDeviceToHost, st);
+  if (e == hipSuccess) e = hipStreamSynchronize(st);
+  release();
+  if (e != hipSuccess) return set_err(EWH_E_HIP, std::string("ewh_optstat: ") + hipGetErrorString(e));
   return 0;
 }
 

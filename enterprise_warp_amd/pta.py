@@ -226,8 +226,10 @@ class PTA:
         """True if some basis depends on theta (chromred 'vary'): no TNT cache."""
         return any(c.basis_groups for c in self._collections)
 
-    def layout(self):
-        """Host-side per-pulsar tables for the engine (plain numpy)."""
+    def layout(self, common_last=None):
+        """Host-side per-pulsar tables for the engine (plain numpy).
+        common_last: name of an uncorrelated GP signal whose columns go last
+        (the optimal-statistic layout, enterprise_warp_amd.optstat)."""
         out = []
         corr = self.correlated()
         for c in self._collections:
@@ -261,8 +263,8 @@ class PTA:
             m = c.T.shape[1]
             ncom = 0
             order = np.arange(m)
-            if corr:
-                com = list(c.common["cols"])
+            if corr or common_last:
+                com = list(c.common["cols"]) if corr else list(c.gp_cols[common_last])
                 if any(j < c.n_lead_const for j in com) or len(set(com)) != len(com):
                     raise ValueError(f"{c.name}: common columns overlap the timing model or each other")
                 own = [j for j in range(m) if j not in set(com)]
@@ -274,7 +276,7 @@ class PTA:
             for j, ents in enumerate(c.entries):
                 for e in ents:
                     if e.get("common"):
-                        continue                      # in the PTA's common descriptor
+                        continue                      # in the PTA's common descriptor (correlated)
                     spec.append(self._spec_tuple(e, int(pos[j])))
             bgroups = [self._pref(p) for p in c.basis_groups]
             out.append(dict(name=c.name, T=np.ascontiguousarray(c.T[:, order], dtype=float), n_common=ncom,
@@ -311,11 +313,13 @@ def _as_ptr(a, ctype):
 class Engine:
     """Owner of one libewarp_hip handle (one device)."""
 
-    def __init__(self, pta, device=0):
+    def __init__(self, pta, device=0, optstat=None):
+        """optstat: None, or {"signal": name, "orf": P x P matrix} for an
+        optimal-statistic handle (ewh_optstat; see enterprise_warp_amd.optstat)."""
         self.lib = _lib.load()
         self.pta = pta
         self.device = device
-        lay = pta.layout()
+        lay = pta.layout(common_last=optstat["signal"] if optstat else None)
         self.n_pulsar = len(lay)
         self.n_param = pta._nparam
         keep = []
@@ -346,14 +350,19 @@ class Engine:
         self.white_fixed = pta.white_fixed() and not pta.basis_varies()
         common = None
         self.correlated = pta.correlated()
-        if self.correlated:
+        if optstat:
+            orf = np.ascontiguousarray(optstat["orf"], dtype=float)
+            keep.append(orf)
+            common = _lib.CommonDesc(L["n_common"], _as_ptr(orf, C.c_double), None, _lib.COMMON_OPTSTAT)
+            keep.append(common)
+        elif self.correlated:
             cl = pta.common_layout()
             cspec = (_lib.SpecEntry * cl["n_col"])()
             for k, (kind, col, p0, p1, p2, f, df) in enumerate(cl["spec"]):
                 cspec[k] = _lib.SpecEntry(kind, col, _lib.Pref(p0[0], 0, p0[1]), _lib.Pref(p1[0], 0, p1[1]),
                                           _lib.Pref(p2[0], 0, p2[1]), f, df, const.fyr)
             keep.extend([cl["orf"], cspec])
-            common = _lib.CommonDesc(cl["n_col"], _as_ptr(cl["orf"], C.c_double), cspec)
+            common = _lib.CommonDesc(cl["n_col"], _as_ptr(cl["orf"], C.c_double), cspec, _lib.COMMON_CORRELATED)
             keep.append(common)
         d = _lib.PtaDesc(_lib.EWH_ABI_VERSION, len(lay), self.n_param, int(self.white_fixed), descs,
                          C.pointer(common) if common is not None else None)
@@ -372,6 +381,21 @@ class Engine:
     def lnl_units_device(self, theta_ptr, B, u0, u1, out_ptr, stream=None):
         _lib.check(self.lib.ewh_lnl_units_device(self.h, C.c_void_p(theta_ptr), int(B), int(u0), int(u1),
                                                  C.c_void_p(out_ptr), C.c_void_p(stream or 0)))
+
+    def optstat(self, theta, phihat, want_pairs=True):
+        """ewh_optstat: (rho [B, P, P], sig [B, P, P], OS [B], OS_sig [B])."""
+        theta = np.ascontiguousarray(theta, dtype=float)
+        phihat = np.ascontiguousarray(phihat, dtype=float)
+        B = theta.shape[0]
+        P = self.n_pulsar
+        rho = np.zeros((B, P, P)) if want_pairs else None
+        sig = np.zeros((B, P, P)) if want_pairs else None
+        os_, os_sig = np.empty(B), np.empty(B)
+        _lib.check(self.lib.ewh_optstat(self.h, _as_ptr(theta, C.c_double), B, _as_ptr(phihat, C.c_double),
+                                        _as_ptr(rho, C.c_double) if want_pairs else None,
+                                        _as_ptr(sig, C.c_double) if want_pairs else None,
+                                        _as_ptr(os_, C.c_double), _as_ptr(os_sig, C.c_double)))
+        return rho, sig, os_, os_sig
 
     def unit_terms(self, B):
         out = np.empty((self.n_pulsar, B))

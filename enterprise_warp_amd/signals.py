@@ -346,6 +346,8 @@ class SignalCollection:
         by_hash = {}       # column bytes -> candidate indices (same result as a linear np.array_equal scan)
         self.col_bgroup_map = {}   # column -> chromatic-index Parameter (theta-dependent basis)
         self.common = None         # correlated common process: {"name", "orf", "cols", "entries"}
+        self.gp_cols = {}          # GP signal name -> its (merged) column indices, in basis order
+        self.gp_entries = {}       # GP signal name -> its spectral entries, same order
         self.n_tm = 0
         seen_gp = False
 
@@ -387,7 +389,9 @@ class SignalCollection:
                             self.common["cols"].append(add(part["F"][:, j], e))
                             self.common["entries"].append(e)
                         elif part["basis_par"] is None:
-                            add(part["F"][:, j], e)
+                            col = add(part["F"][:, j], e)
+                            self.gp_cols.setdefault(b.name, []).append(col)
+                            self.gp_entries.setdefault(b.name, []).append(e)
                         else:   # theta-dependent basis: own column, never merged
                             cols.append(part["F"][:, j])
                             entries.append([e])

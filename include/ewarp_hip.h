@@ -49,7 +49,7 @@
 extern "C" {
 #endif
 
-#define EWH_ABI_VERSION 3
+#define EWH_ABI_VERSION 4
 
 enum ewh_status {
   EWH_OK = 0,
@@ -131,10 +131,18 @@ typedef struct ewh_pulsar_desc {
  * column g of pulsar b by orf[a][b] * phi_common(g); the pulsars' own
  * signals add to the diagonal.  Requires fixed white noise (this ABI
  * version). */
+enum ewh_common_kind {
+  EWH_COMMON_CORRELATED = 0,    /* correlated common process in the likelihood */
+  EWH_COMMON_OPTSTAT = 1        /* optimal statistic of an uncorrelated (CURN) model, see ewh_optstat */
+};
+
 typedef struct ewh_common_desc {
   int32_t n_col;                /* common columns per pulsar (2 x frequencies), <= 31 */
   const double* orf;            /* n_pulsar x n_pulsar, row-major: Gamma_ab (diagonal included) */
-  const ewh_spec_entry* spec;   /* n_col entries, spec[g].col = g: phi_common of column g */
+  const ewh_spec_entry* spec;   /* CORRELATED: n_col entries, spec[g].col = g: phi_common of column g.
+                                 * OPTSTAT: unused (the common signal's entries are part of each
+                                 * pulsar's own spec list, as in the CURN likelihood) */
+  int32_t kind;                 /* ewh_common_kind */
 } ewh_common_desc;
 
 typedef struct ewh_pta_desc {
@@ -164,6 +172,19 @@ int ewh_lnl_batch(ewh_handle* h, const double* theta_host, int32_t B, double* ou
 int ewh_lnl_units_device(ewh_handle* h, const double* theta_dev, int32_t B,
                          int64_t unit_begin, int64_t unit_end, double* out_dev,
                          void* stream);
+
+/* Optimal statistic (the reference's results.py:653-795 ->
+ * enterprise_extensions OptimalStatistic.compute_os) for B noise-parameter
+ * draws, on a handle created with common->kind == EWH_COMMON_OPTSTAT (fixed
+ * white noise): per pulsar X = F^T P^-1 r, Z = F^T P^-1 F (F = the common
+ * columns, P = N + T phi T^T with the common process included), per pair
+ * rho_ab = X_a^T phihat X_b / tr(Z_a phihat Z_b phihat), sig_ab = tr(..)^-1/2,
+ * OS = sum rho Gamma / sig^2 / sum Gamma^2 / sig^2, OS_sig = (sum Gamma^2/sig^2)^-1/2.
+ * theta_host [B x n_param]; phihat_host [B x n_col] (unit-amplitude spectrum
+ * per draw); rho_host / sig_host [B x n_pulsar x n_pulsar] (pairs a < b
+ * filled; may be NULL); os_host, os_sig_host [B]. Synchronous. */
+int ewh_optstat(ewh_handle* h, const double* theta_host, int32_t B, const double* phihat_host,
+                double* rho_host, double* sig_host, double* os_host, double* os_sig_host);
 
 /* Per-pulsar lnL terms of the last call: out_host [n_pulsar x B] (row p =
  * pulsar p).  Units outside the last range read 0. Synchronous. */

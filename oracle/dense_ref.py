@@ -106,3 +106,30 @@ def woodbury_lnl_pta(oracle_pta, params, tm_var):
     x = sl.cho_solve(cf, d)
     return (-0.5 * sum(t[2] + t[3] for t in terms)
             + 0.5 * (d @ x - 2 * np.sum(np.log(np.diag(cf[0]))) - logdet_phi))
+
+
+def dense_os_xz(oracle_pulsar, params, gw_name="gw"):
+    """X = F^T C^-1 r and Z = F^T C^-1 F of the optimal statistic from the
+    dense covariance (enterprise_extensions OptimalStatistic.get_XZ computes
+    the same through Woodbury).  C = N + T_gp phi T_gp^T + M phi_tm M^T is
+    taken in the limit phi_tm -> inf (the 1e40 of [ent] utils.tm_prior):
+    C^-1 = A - A M (M^T A M)^-1 M^T A with A = (N + T_gp phi T_gp^T)^-1."""
+    pp = oracle_pulsar
+    D, ep = pp._sm(params)
+    C = np.diag(D)
+    for slc, jv in ep:
+        C[slc, slc] += jv
+    phi = pp.phi(params)
+    T = pp.basis(params)
+    tm = np.zeros(T.shape[1], bool)
+    for g in pp.gps:
+        if g["kind"] == "tm":
+            tm[g["idx"]] = True
+    C += (T[:, ~tm] * phi[None, ~tm]) @ T[:, ~tm].T
+    A = sl.cho_solve(sl.cho_factor(C), np.eye(len(D)))
+    M = T[:, tm]
+    AM = A @ M
+    Cinv = A - AM @ np.linalg.solve(M.T @ AM, AM.T)
+    g = next(g for g in pp.gps if g.get("name") == gw_name)
+    F = T[:, np.asarray(g["idx"])]
+    return F.T @ Cinv @ pp.r, F.T @ Cinv @ F

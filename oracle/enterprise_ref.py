@@ -500,3 +500,51 @@ class OraclePTA:
         loglike += -0.5 * np.sum([ell for ell in rnr_ld])
         loglike += red
         return loglike
+
+
+
+# --------------------------------------------------------------------------
+# optimal statistic (results.py:653-795 -> enterprise_extensions
+# frequentist.optimal_statistic.OptimalStatistic, unpinned, absent)
+# --------------------------------------------------------------------------
+def optimal_statistic(opta, params, gw_name="gw", orf="hd", gamma=None):
+    """Restates enterprise_extensions OptimalStatistic.get_XZ + compute_os on
+    the CURN model: per pulsar, with P = N + T phi T^T (the common process
+    included, as the noise-marginalised OS of results.py uses the CURN chain),
+      X = F^T P^-1 r,  Z = F^T P^-1 F   (F = the common signal's columns),
+    then per pair rho_ab = X_a^T phi^ X_b / tr(Z_a phi^ Z_b phi^),
+    sig_ab = tr(...)^-1/2 with phi^ the unit-amplitude power law, and
+    OS = sum rho Gamma / sig^2 / sum Gamma^2 / sig^2, OS_sig = (sum Gamma^2 / sig^2)^-1/2.
+    gamma: params['gw_gamma'] when None (13/3 if absent).  Returns
+    (xi, rho, sig, OS, OS_sig) over pairs a < b in row-major order."""
+    if gamma is None:
+        gamma = params.get("gw_gamma", 13.0 / 3.0)
+    Xs, Zs, pos, freqs = [], [], [], None
+    for i, pp in enumerate(opta.pulsars):
+        TNT, TNr, _, _ = opta.fixed[i] if opta.fixed is not None else pp.white_terms(params)
+        phi = pp.phi(params)
+        g = next(g for g in pp.gps if g.get("name") == gw_name)
+        idx = np.asarray(g["idx"])
+        freqs = g["f"]
+        Sigma = TNT + np.diag(1.0 / phi)
+        cf = sl.cho_factor(Sigma)
+        SigmaTNr = sl.cho_solve(cf, TNr)
+        FNT = TNT[idx, :]
+        SigmaTNF = sl.cho_solve(cf, FNT.T)
+        Xs.append(TNr[idx] - FNT @ SigmaTNr)
+        Zs.append(TNT[np.ix_(idx, idx)] - FNT @ SigmaTNF)
+        pos.append(np.asarray(pp.psr.pos, float))
+    phat = powerlaw(freqs, 0.0, gamma, 2)
+    xi, rho, sig, G = [], [], [], []
+    P = len(Xs)
+    for a in range(P):
+        for b in range(a + 1, P):
+            top = Xs[a] @ (phat * Xs[b])
+            bot = np.trace((Zs[a] * phat[None, :]) @ (Zs[b] * phat[None, :]))
+            rho.append(top / bot)
+            sig.append(1.0 / np.sqrt(bot))
+            G.append(orf_value(orf, pos[a], pos[b]))
+            xi.append(np.arccos(np.clip(np.dot(pos[a], pos[b]), -1, 1)))
+    rho, sig, G, xi = map(np.array, (rho, sig, G, xi))
+    OS = np.sum(rho * G / sig ** 2) / np.sum(G ** 2 / sig ** 2)
+    return xi, rho, sig, OS, 1.0 / np.sqrt(np.sum(G ** 2 / sig ** 2))
