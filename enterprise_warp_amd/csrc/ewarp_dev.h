@@ -501,10 +501,12 @@ __device__ __forceinline__ void static_for(F&& f) {
   }
 }
 
-// A -= U_i^T U_j : four f64 MFMAs (A operand = -U_i)
+// A -= U_i^T U_j : four f64 MFMAs.  For the f64 MFMAs of gfx940+ the last
+// (blgp) field is the neg modifier (bit 0 negates A: `neg:[1,0,0]`), so no
+// v_xor per negated operand.
 __device__ __forceinline__ void syrk_update(v4d& C, const v4d& Ui, const v4d& Uj) {
 #pragma unroll
-  for (int sk = 0; sk < 4; ++sk) C = __builtin_amdgcn_mfma_f64_16x16x4f64(-Ui[sk], Uj[sk], C, 0, 0, 0);
+  for (int sk = 0; sk < 4; ++sk) C = __builtin_amdgcn_mfma_f64_16x16x4f64(Ui[sk], Uj[sk], C, 0, 0, 1);
 }
 
 // FULL: 1 = every panel step unrolled (large code), 0 = runtime loop over the
@@ -524,12 +526,22 @@ __device__ __forceinline__ void syrk_update(v4d& C, const v4d& Ui, const v4d& Uj
 // pivots are factored by VALU (ALG 1: row k broadcast by ds_bpermute, ALG 2:
 // through the per-wave LDS `rowbuf`), then the block row is scaled to
 // U = D^-1/2 V.  Accumulates log d_k (one lane per row) and d_k > 0 per lane.
-// lane (q, c) <- lane (q, K) of its 16-lane row (DPP row_newbcast, gfx90a+)
+// lane (q, c) <- lane (q, K) of its 16-lane row (DPP row_newbcast, gfx90a+):
+// one v_mov_b64_dpp (64-bit DPP takes row_newbcast).  mov_dpp with bound_ctrl
+// has no `old` operand, so no zero is materialised per move (update_dpp(0, ...)
+// on two 32-bit halves cost 2 DPP + 2 v_mov per double).
 template <int K>
 __device__ __forceinline__ double row_newbcast(double x) {
-  const int lo = __builtin_amdgcn_update_dpp(0, __double2loint(x), 0x150 + K, 0xf, 0xf, false);
-  const int hi = __builtin_amdgcn_update_dpp(0, __double2hiint(x), 0x150 + K, 0xf, 0xf, false);
-  return __hiloint2double(hi, lo);
+  const long v = __builtin_amdgcn_mov_dpp(__builtin_bit_cast(long, x), 0x150 + K, 0xf, 0xf, true);
+  return __builtin_bit_cast(double, v);
+}
+
+// the same, only into the 16-lane rows selected by RM (bit q = row q); the
+// other rows read 0 (the `old` operand)
+template <int K, int RM>
+__device__ __forceinline__ double row_newbcast_rows(double x) {
+  const long v = __builtin_amdgcn_update_dpp(0L, __builtin_bit_cast(long, x), 0x150 + K, RM, 0xf, false);
+  return __builtin_bit_cast(double, v);
 }
 
 template <int NB, int FULL, int ALG, typename BBt, typename Blk>
@@ -539,7 +551,60 @@ __device__ __forceinline__ void panel_ldl_row(BBt BBc, Blk&& blk, int q, int c, 
   (void)rowbuf;
   (void)LD;
   constexpr int bb = decltype(BBc)::value;
-  static_assert(ALG != 3 || FULL, "the DPP panel needs compile-time pivots");
+  static_assert(ALG < 3 || FULL, "the DPP panel needs compile-time pivots");
+  if constexpr (ALG == 5) {
+    // ALG 5 (blocked panel): eliminate the 16x16 diagonal block alone (rows >
+    // k take row k, u_i from its symmetric lower part by DPP as ALG 3/4)
+    // while E = L^-T accumulates the matching COLUMN operations
+    //   col c -= u_c col k  (c > k),  u_c = A[k][c] / d_k = rk_bb[c] / d_k
+    // (column k of E is an intra-row DPP broadcast, u_c is the row-k value
+    // this lane already holds: no LDS).  The off-diagonal blocks of the row
+    // then take V_bj = L^-1 A_bj = E^T A_bj by four MFMAs each instead of 16
+    // rank-1 VALU steps and 16 row broadcasts (2 ds_bpermute per double).
+    v4d E;
+    static_for<0, 4>([&](auto R) {
+      constexpr int r = decltype(R)::value;
+      E[r] = (q + 4 * r == c) ? 1.0 : 0.0;
+    });
+    static_for<0, 4>([&](auto KR) {
+      constexpr int kr = decltype(KR)::value;
+      constexpr int nk = (bb == NB - 1 && kr == 3) ? 3 : 4;   // the r column is not pivoted
+      static_for<0, nk>([&](auto KQc) {
+        constexpr int kq = decltype(KQc)::value;
+        constexpr int k = 4 * kr + kq;
+        const double d = readlane_d(blk(BBc)[kr], 16 * kq + k);
+        // raw multipliers A[q + 4r][k] (rows > k): register kr only in the
+        // 16-lane rows q > kq (DPP row_mask; disabled rows read 0)
+        double ui[4];
+        static_for<kr + 1, 4>([&](auto R) {
+          constexpr int r = decltype(R)::value;
+          ui[r] = row_newbcast<k>(blk(BBc)[r]);
+        });
+        if constexpr (kq < 3) ui[kr] = row_newbcast_rows<k, (0xf << (kq + 1)) & 0xf>(blk(BBc)[kr]);
+        // w = A[k][c] / d_k: the row-k value of this lane's column, scaled once
+        const double w = __shfl(blk(BBc)[kr], 16 * kq + c) * rcp_nr(d);
+        static_for<(kq < 3 ? kr : kr + 1), 4>([&](auto R) {
+          constexpr int r = decltype(R)::value;
+          blk(BBc)[r] = fma(-ui[r], w, blk(BBc)[r]);
+        });
+        if constexpr (bb < NB - 1 && k < 15) {
+          const double uc = (c > k) ? w : 0.0;
+          static_for<0, kr + 1>([&](auto R) {
+            constexpr int r = decltype(R)::value;
+            E[r] = fma(-uc, row_newbcast<k>(E[r]), E[r]);
+          });
+        }
+      });
+    });
+    static_for<bb + 1, NB>([&](auto JJ) {
+      v4d acc = {0.0, 0.0, 0.0, 0.0};
+      static_for<0, 4>([&](auto S) {
+        constexpr int s = decltype(S)::value;
+        acc = __builtin_amdgcn_mfma_f64_16x16x4f64(E[s], blk(JJ)[s], acc, 0, 0, 0);
+      });
+      blk(JJ) = acc;
+    });
+  } else
   static_for<0, 4>([&](auto KR) {
     constexpr int kr = decltype(KR)::value;
     // ALG 3: u_i = A[q + 4r][k] read from the SYMMETRIC lower part of the
@@ -554,7 +619,7 @@ __device__ __forceinline__ void panel_ldl_row(BBt BBc, Blk&& blk, int q, int c, 
       static_for<kr, 4>([&](auto R) {
         constexpr int r = decltype(R)::value;
         const double v = row_newbcast<k>(blk(BBc)[r]);
-        ui[r] = (r > kr || q > kq) ? v : 0.0;
+        ui[r] = (ALG == 4 || r > kr || q > kq) ? v : 0.0;
       });
       static_for<bb, NB>([&](auto JJ) {
         constexpr int j = decltype(JJ)::value;
@@ -564,11 +629,21 @@ __device__ __forceinline__ void panel_ldl_row(BBt BBc, Blk&& blk, int q, int c, 
       static_for<kr, 4>([&](auto R) { ui[decltype(R)::value] *= dinv; });
       static_for<bb, NB>([&](auto JJ) {
         constexpr int j = decltype(JJ)::value;
-        static_for<kr, 4>([&](auto R) {
+        static_for<(ALG == 4 ? kr + 1 : kr), 4>([&](auto R) {
           constexpr int r = decltype(R)::value;
           blk(JJ)[r] = fma(-ui[r], rk[j], blk(JJ)[r]);
         });
       });
+      // ALG 4: register kr holds rows 4 kr + q and only rows below the pivot
+      // (q > kq) change -- an exec-masked branch (SALU) instead of a select on u_i
+      if constexpr (ALG == 4) {
+        if (q > kq) {
+          static_for<bb, NB>([&](auto JJ) {
+            constexpr int j = decltype(JJ)::value;
+            blk(JJ)[kr] = fma(-ui[kr], rk[j], blk(JJ)[kr]);
+          });
+        }
+      }
     };
     auto step = [&](const int kq) {
       const int k = 4 * kr + kq;
@@ -625,7 +700,7 @@ __device__ __forceinline__ void panel_ldl_row(BBt BBc, Blk&& blk, int q, int c, 
       });
     };
     constexpr int nk = (bb == NB - 1 && kr == 3) ? 3 : 4;   // the r column is not pivoted
-    if constexpr (ALG == 3) {
+    if constexpr (ALG >= 3) {
       static_for<0, nk>([&](auto KQ) { step3(KQ); });
     } else if constexpr (FULL) {
       static_for<0, nk>([&](auto KQ) {

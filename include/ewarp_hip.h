@@ -194,13 +194,17 @@ int ewh_last_unit_terms(ewh_handle* h, double* out_host, int32_t B);
 double ewh_unit_cost(const ewh_handle* h, int32_t pulsar);
 
 /* Kernel selection: 0 = auto (register-blocked MFMA factorisation with the
- * LDL^T panel when the reduced matrix fits, LDS kernel otherwise), 1 = force
- * the LDS kernel, 2 = the round-1 MFMA kernel (Cholesky panel, looped steps).
- * A/B variants for NB = 8 only (else as 0): 3 = LDL^T at one wave per SIMD,
- * 4 = LDL^T with looped steps, 5 = LDL^T with u_i by ds_bpermute (unrolled),
- * 6 = LDL^T with the row broadcast through LDS.  7 = default Cholesky with
- * the round-1 contraction (varying white noise: separate epoch-sum kernel,
- * unpipelined tiles) instead of the pipelined one. */
+ * LDL^T panel when the reduced matrix fits -- up to NB = 8 the blocked panel:
+ * diagonal block by VALU, the rest of the block row by MFMA with L^-1 --, LDS
+ * kernel otherwise), 1 = force the LDS kernel, 2 = the round-1 MFMA kernel
+ * (Cholesky panel, looped steps).  A/B variants for NB = 8 only (else as 0):
+ * 3 = unblocked DPP panel at one wave per SIMD, 4 = LDL^T with looped steps,
+ * 5 = LDL^T with u_i by ds_bpermute (unrolled), 6 = LDL^T with the row
+ * broadcast through LDS, 8 = unblocked DPP panel with the pivot row's own
+ * update exec-masked, 9 = unblocked DPP panel (every block of the row by
+ * VALU).  7 = default Cholesky with the round-1 contraction (varying white
+ * noise: separate epoch-sum kernel, unpipelined tiles) instead of the
+ * pipelined one. */
 int ewh_set_kernel_mode(ewh_handle* h, int32_t mode);
 
 void ewh_destroy(ewh_handle* h);
