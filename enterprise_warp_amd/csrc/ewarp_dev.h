@@ -484,7 +484,10 @@ template <int NB>
 struct Split {
   // block rows of phase 1: NB/2, except 3 of 8 (phase 1's 21 blocks + panel
   // temporaries then fit 256 VGPRs without spills; phase 2 runs row by row)
-  static constexpr int H = NB == 8 ? 3 : NB / 2;
+#ifndef EWH_H8
+#define EWH_H8 3
+#endif
+  static constexpr int H = NB == 8 ? EWH_H8 : NB / 2;
   static constexpr int M = NB - H;                    // A22 block order
   static constexpr int n1 = H * NB - H * (H - 1) / 2; // blocks (i < H, j >= i)
   static constexpr int n2 = M * (M + 1) / 2;          // blocks (H <= i <= j)
@@ -764,7 +767,11 @@ void chol_mfma_kernel(const CholJob* __restrict__ jobs, int B, long long u0, int
     }
     phinv[a] = pi;
   }
-  const double lphi_sum = wave_sum(lphi.value());
+  // ALG >= 1 sums log|phi| into the per-lane log-det accumulator below, so
+  // the kernel takes a single log() at its end (two calls let the compiler
+  // keep the polynomial constants of the first one live across the whole
+  // factorisation: spilled to scratch and reloaded serially at the end)
+  const double lphi_sum = ALG >= 1 ? 0.0 : wave_sum(lphi.value());
   __syncthreads();
 
   auto load_block = [&](auto BI, auto BJ, v4d& v) {
@@ -783,6 +790,7 @@ void chol_mfma_kernel(const CholJob* __restrict__ jobs, int B, long long u0, int
   };
 
   LogAcc ldet;
+  if constexpr (ALG >= 1) ldet = lphi;
   bool ok = true;
   // LDL^T panel row bb (ALG >= 1)
   auto panel_ldl = [&](auto BBc, auto&& blk) {
