@@ -406,12 +406,20 @@ __device__ __forceinline__ void contract2_body(const PsrDev& P, const double* __
         });
       }
       if (pass == 0 && ecorr && tid < LD) {          // epoch sums of column tid
+        // the tile's 32 values of the column are read up front (independent
+        // LDS loads, one round trip) and the epoch flags are wave-uniform
+        // (readfirstlane: scalar branches), so the running sum is a chain of
+        // FMAs instead of a dependent LDS read + branch per row
         const double* tcol = tile + tid;
         const int* ecur = ebase + cur * CT_ROWS;
+        double tc[CT_ROWS];
+#pragma unroll
+        for (int r = 0; r < CT_ROWS; ++r) tc[r] = tcol[r * LD];
+#pragma unroll
         for (int r = 0; r < CT_ROWS; ++r) {
-          const int e = ecur[r];
+          const int e = __builtin_amdgcn_readfirstlane(ecur[r]);
           if (e >= 0) {
-            eacc = fma(wt[r], tcol[r * LD], eacc);
+            eacc = fma(wt[r], tc[r], eacc);
             if (e & 1) {
               srow[(long long)(e >> 1) * LD + tid] = eacc;
               eacc = 0.0;
@@ -480,14 +488,13 @@ __global__ __launch_bounds__(256) void contract2_kernel(PsrDev P, const double* 
 // triangle and apply the H panel rows to it; (3) factor A22.  Same
 // arithmetic, re-ordered (left-looking at the 2x2 block level).
 // ----------------------------------------------------------------------------
-template <int NB>
+template <int NB, int ALG = 0>
 struct Split {
-  // block rows of phase 1: NB/2, except 3 of 8 (phase 1's 21 blocks + panel
-  // temporaries then fit 256 VGPRs without spills; phase 2 runs row by row)
-#ifndef EWH_H8
-#define EWH_H8 3
-#endif
-  static constexpr int H = NB == 8 ? EWH_H8 : NB / 2;
+  // block rows of phase 1: NB/2, except 3 of 8 for the unblocked panels
+  // (phase 1's 21 blocks + panel temporaries then fit 256 VGPRs without
+  // spills; phase 2 runs row by row).  The blocked panel (ALG 5) has fewer
+  // panel temporaries and fits at NB/2 = 4 with no scratch (3 spills).
+  static constexpr int H = (NB == 8 && ALG != 5) ? 3 : NB / 2;
   static constexpr int M = NB - H;                    // A22 block order
   static constexpr int n1 = H * NB - H * (H - 1) / 2; // blocks (i < H, j >= i)
   static constexpr int n2 = M * (M + 1) / 2;          // blocks (H <= i <= j)
@@ -743,7 +750,7 @@ void chol_mfma_kernel(const CholJob* __restrict__ jobs, int B, long long u0, int
                       const double* __restrict__ theta, int ldth, double* __restrict__ out_units,
                       double* __restrict__ keep_out, int keep_b0, int keep_P) {
   constexpr int LD = 16 * NB;
-  using S = Split<NB>;
+  using S = Split<NB, ALG>;
   constexpr int H = S::H;
   static_assert(NB - KEEP >= H, "kept blocks must lie in the phase-3 triangle");
   __shared__ double phinv[LD];
