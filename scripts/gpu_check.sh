@@ -26,5 +26,5 @@ run bench 600 python bench.py --steps 10 --warmup 2
 run chol_ab 600 python scripts/chol_ab.py --rounds 5 --modes 0,3,2
 run configs 900 python scripts/bench_configs.py
 run pmc 1500 bash scripts/gpu_pmc.sh $TAG
-run rocprof 600 rocprofv3 --kernel-trace --stats -d gpurun_out/prof_$TAG -o run --output-format csv -- python bench.py --steps 5 --warmup 1 --no-cpu-baseline
+run rocprof 600 rocprofv3 --kernel-trace --stats -d gpurun_out/prof_$TAG -o run --output-format csv -- python bench.py --steps 20 --warmup 3 --no-cpu-baseline
 echo ALL_DONE
