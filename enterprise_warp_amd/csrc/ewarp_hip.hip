@@ -275,6 +275,113 @@ __global__ __launch_bounds__(256) void common_minv_kernel(const CommonPsr* __res
   if (threadIdx.x == 0) mlog[(long long)bl * nc + slot] = ok ? lsum : __builtin_nan("");
 }
 
+// The same inverse for P <= MINV_PMAX with M held in registers: wave w owns
+// rows i = w + 4 r (r < MINV_PMAX / 4), lane l columns j = l + 64 cc (cc < 2).
+// Per pivot k the owners of column k and row k publish them to LDS (double
+// buffered by pivot parity: one barrier per pivot) and every thread updates
+// its elements in place -- no integer division or LDS round trip per element
+// (the LDS version above costs ~30x more on C5's 100 x 100 blocks).
+constexpr int MINV_PMAX = 128;
+
+__global__ __launch_bounds__(256) void common_minv_reg_kernel(const CommonPsr* __restrict__ cps, int P,
+                                                              const double* __restrict__ orf,
+                                                              const DSpec* __restrict__ cspec, int nc,
+                                                              const int* __restrict__ uniq,
+                                                              const double* __restrict__ theta, int ldth, int b0,
+                                                              double* __restrict__ minv, double* __restrict__ mlog) {
+  constexpr int RW = MINV_PMAX / 4;     // rows per wave
+  __shared__ double own[MINV_PMAX];
+  __shared__ double colk[2][MINV_PMAX], rowk[2][MINV_PMAX];
+  const int tid = threadIdx.x, w = tid >> 6, lane = tid & 63;
+  const int slot = blockIdx.x, g = uniq[slot], bl = blockIdx.y;
+  const double* th = theta + (long long)(b0 + bl) * ldth;
+  const double pc = spec_phi(cspec[g], th);
+  for (int a = tid; a < P; a += 256) {
+    const CommonPsr c = cps[a];
+    double v = 0.0;
+    for (int e = c.colptr[c.gstart + g]; e < c.colptr[c.gstart + g + 1]; ++e) v += spec_phi(c.spec[e], th);
+    own[a] = v;
+  }
+  __syncthreads();
+  double m[RW][2];
+#pragma unroll
+  for (int r = 0; r < RW; ++r) {
+    const int i = w + 4 * r;
+#pragma unroll
+    for (int cc = 0; cc < 2; ++cc) {
+      const int j = lane + 64 * cc;
+      m[r][cc] = (i < P && j < P) ? orf[i * P + j] * pc + (i == j ? own[i] : 0.0) : 0.0;
+    }
+  }
+  LogAcc lacc;
+  bool ok = true;
+  for (int k = 0; k < P; ++k) {
+    const int buf = k & 1;
+    if (lane == (k & 63)) {               // column k: this lane, slot k / 64
+      const bool hi = k >= 64;
+#pragma unroll
+      for (int r = 0; r < RW; ++r) colk[buf][w + 4 * r] = hi ? m[r][1] : m[r][0];
+    }
+    if (w == (k & 3)) {                   // row k: this wave, register k / 4
+      const int rk = k >> 2;
+#pragma unroll
+      for (int r = 0; r < RW; ++r)
+        if (r == rk) {
+          rowk[buf][lane] = m[r][0];
+          rowk[buf][lane + 64] = m[r][1];
+        }
+    }
+    __syncthreads();
+    const double piv = rowk[buf][k];
+    ok = ok && (piv > 0.0);
+    lacc.add(piv);
+    const double pinv = 1.0 / piv;
+    const double rj0 = rowk[buf][lane] * pinv, rj1 = rowk[buf][lane + 64] * pinv;
+    double ci[RW];
+#pragma unroll
+    for (int r = 0; r < RW; ++r) {
+      ci[r] = colk[buf][w + 4 * r];
+      m[r][0] = fma(-ci[r], rj0, m[r][0]);
+      m[r][1] = fma(-ci[r], rj1, m[r][1]);
+    }
+    // column k (one lane per wave): -M[i][k] / piv; then row k: M[k][j] / piv
+    // and the pivot 1 / piv (uniform branches on k, one divergent lane test)
+    if (lane == (k & 63)) {
+      if (k < 64) {
+#pragma unroll
+        for (int r = 0; r < RW; ++r) m[r][0] = -ci[r] * pinv;
+      } else {
+#pragma unroll
+        for (int r = 0; r < RW; ++r) m[r][1] = -ci[r] * pinv;
+      }
+    }
+    if (w == (k & 3)) {
+      const int rk = k >> 2;
+#pragma unroll
+      for (int r = 0; r < RW; ++r)
+        if (r == rk) {
+          m[r][0] = rj0;
+          m[r][1] = rj1;
+          if (lane == (k & 63)) {
+            if (k < 64) m[r][0] = pinv;
+            else m[r][1] = pinv;
+          }
+        }
+    }
+  }
+  double* out = minv + ((long long)bl * nc + slot) * P * P;
+#pragma unroll
+  for (int r = 0; r < RW; ++r) {
+    const int i = w + 4 * r;
+#pragma unroll
+    for (int cc = 0; cc < 2; ++cc) {
+      const int j = lane + 64 * cc;
+      if (i < P && j < P) out[i * P + j] = m[r][cc];
+    }
+  }
+  if (tid == 0) mlog[(long long)bl * nc + slot] = ok ? lacc.value() : __builtin_nan("");
+}
+
 // Dense Sigma_c (Np x Np, row-major) of sample bl, one row per workgroup:
 // rows/cols (a, g) -> a nc + g; r at Np - 1; pad rows/cols identity.
 __global__ __launch_bounds__(256) void common_assemble_kernel(const double* __restrict__ keep, int KD, int P, int nc,
@@ -1103,8 +1210,12 @@ int lnl_correlated(ewh_handle* h, const double* theta_dev, int B, hipStream_t st
   const size_t lds = ((size_t)P * (P + 1) + 3 * P) * sizeof(double);
   for (int c0 = 0; c0 < B; c0 += h->cchunk) {
     const int nb = std::min(h->cchunk, B - c0);
-    hipLaunchKernelGGL(common_minv_kernel, dim3(h->nuniq, nb), dim3(256), lds, st, h->d_cps, P, h->d_orf,
-                       h->d_cspec, h->nc, h->d_cuniq, theta_dev, ldth, c0, h->d_minv, h->d_mlog);
+    if (P <= MINV_PMAX && h->kernel_mode != 7)
+      hipLaunchKernelGGL(common_minv_reg_kernel, dim3(h->nuniq, nb), dim3(256), 0, st, h->d_cps, P, h->d_orf,
+                         h->d_cspec, h->nc, h->d_cuniq, theta_dev, ldth, c0, h->d_minv, h->d_mlog);
+    else
+      hipLaunchKernelGGL(common_minv_kernel, dim3(h->nuniq, nb), dim3(256), lds, st, h->d_cps, P, h->d_orf,
+                         h->d_cspec, h->nc, h->d_cuniq, theta_dev, ldth, c0, h->d_minv, h->d_mlog);
     hipLaunchKernelGGL(common_assemble_kernel, dim3(h->Np, nb), dim3(256), 0, st,
                        h->d_keep + (size_t)c0 * P * KD * KD, KD, P, h->nc, h->d_minv, h->d_crep, h->Np,
                        h->d_dense);

@@ -202,9 +202,10 @@ double ewh_unit_cost(const ewh_handle* h, int32_t pulsar);
  * 5 = LDL^T with u_i by ds_bpermute (unrolled), 6 = LDL^T with the row
  * broadcast through LDS, 8 = unblocked DPP panel with the pivot row's own
  * update exec-masked, 9 = unblocked DPP panel (every block of the row by
- * VALU).  7 = default Cholesky with the round-1 contraction (varying white
- * noise: separate epoch-sum kernel, unpipelined tiles) instead of the
- * pipelined one. */
+ * VALU).  7 = default Cholesky with the round-1 kernels elsewhere: the
+ * contraction (varying white noise: separate epoch-sum kernel, unpipelined
+ * tiles) instead of the pipelined one and, for a correlated common process,
+ * the right-looking dense update and the LDS Gauss-Jordan M_g inverse. */
 int ewh_set_kernel_mode(ewh_handle* h, int32_t mode);
 
 void ewh_destroy(ewh_handle* h);
