@@ -142,6 +142,27 @@ __device__ __forceinline__ double rcp_nr(double a) {
   return fma(y, e, y);
 }
 
+// x / a with one cubic correction: y = rcp(a) (|e| = |1 - a y| < 2^-24),
+// x / a = x y (1 + e + e^2) + O(e^3).  t = x y forms beside e, so the chain
+// after the estimate is e -> s -> result (3 ops; x * rcp_nr(a) is 5) and the
+// whole quotient is 5 fp64 VALU ops instead of 6.  ~1 ulp.
+__device__ __forceinline__ double div_fast(double x, double a) {
+  const double y = __builtin_amdgcn_rcp(a);
+  const double e = fma(-a, y, 1.0);
+  const double t = x * y;
+  const double s = fma(e, e, e);
+  return fma(t, s, t);
+}
+
+// 1/sqrt(a) with one cubic correction: e = 1 - a y^2,
+// a^-1/2 = y (1 + e/2 + 3e^2/8) + O(e^3).  6 fp64 VALU ops (rsqrt_nr is 8).
+__device__ __forceinline__ double rsqrt_fast(double a) {
+  const double y = __builtin_amdgcn_rsq(a);
+  const double e = fma(-(a * y), y, 1.0);
+  const double s = e * fma(0.375, e, 0.5);
+  return fma(y, s, y);
+}
+
 __device__ __forceinline__ double wave_sum(double v) {
 #pragma unroll
   for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o);
@@ -494,7 +515,7 @@ struct Split {
   // (phase 1's 21 blocks + panel temporaries then fit 256 VGPRs without
   // spills; phase 2 runs row by row).  The blocked panel (ALG 5) has fewer
   // panel temporaries and fits at NB/2 = 4 with no scratch (3 spills).
-  static constexpr int H = (NB == 8 && ALG != 5) ? 3 : NB / 2;
+  static constexpr int H = (NB == 8 && ALG < 5) ? 3 : NB / 2;
   static constexpr int M = NB - H;                    // A22 block order
   static constexpr int n1 = H * NB - H * (H - 1) / 2; // blocks (i < H, j >= i)
   static constexpr int n2 = M * (M + 1) / 2;          // blocks (H <= i <= j)
@@ -562,7 +583,7 @@ __device__ __forceinline__ void panel_ldl_row(BBt BBc, Blk&& blk, int q, int c, 
   (void)LD;
   constexpr int bb = decltype(BBc)::value;
   static_assert(ALG < 3 || FULL, "the DPP panel needs compile-time pivots");
-  if constexpr (ALG == 5) {
+  if constexpr (ALG >= 5) {
     // ALG 5 (blocked panel): eliminate the 16x16 diagonal block alone (rows >
     // k take row k, u_i from its symmetric lower part by DPP as ALG 3/4)
     // while E = L^-T accumulates the matching COLUMN operations
@@ -592,7 +613,11 @@ __device__ __forceinline__ void panel_ldl_row(BBt BBc, Blk&& blk, int q, int c, 
         });
         if constexpr (kq < 3) ui[kr] = row_newbcast_rows<k, (0xf << (kq + 1)) & 0xf>(blk(BBc)[kr]);
         // w = A[k][c] / d_k: the row-k value of this lane's column, scaled once
-        const double w = __shfl(blk(BBc)[kr], 16 * kq + c) * rcp_nr(d);
+        // (ALG >= 6: the quotient by div_fast -- one op and ~12 cycles of the
+        // per-pivot chain less; ALG 6 also scales the rows by rsqrt_fast,
+        // which makes this kernel spill 68 bytes per lane, ALG 7 does not)
+        const double xk = __shfl(blk(BBc)[kr], 16 * kq + c);
+        const double w = ALG >= 6 ? div_fast(xk, d) : xk * rcp_nr(d);
         static_for<(kq < 3 ? kr : kr + 1), 4>([&](auto R) {
           constexpr int r = decltype(R)::value;
           blk(BBc)[r] = fma(-ui[r], w, blk(BBc)[r]);
@@ -734,7 +759,7 @@ __device__ __forceinline__ void panel_ldl_row(BBt BBc, Blk&& blk, int q, int c, 
     const double dv = rrow ? 1.0 : dg;
     ok = ok && (dv > 0.0);
     if (c == 0) ldet.add(dv);
-    const double rs = rrow ? 1.0 : rsqrt_nr(dv);
+    const double rs = rrow ? 1.0 : (ALG == 6 ? rsqrt_fast(dv) : rsqrt_nr(dv));
     static_for<bb, NB>([&](auto JJ) { blk(JJ)[r] *= rs; });
   });
 }

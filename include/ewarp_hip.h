@@ -202,7 +202,9 @@ double ewh_unit_cost(const ewh_handle* h, int32_t pulsar);
  * 5 = LDL^T with u_i by ds_bpermute (unrolled), 6 = LDL^T with the row
  * broadcast through LDS, 8 = unblocked DPP panel with the pivot row's own
  * update exec-masked, 9 = unblocked DPP panel (every block of the row by
- * VALU).  7 = default Cholesky with the round-1 kernels elsewhere: the
+ * VALU), 10 = blocked panel with the quotients by two Newton steps on the
+ * hardware rcp estimate (the default uses one cubic correction), 11 = the
+ * default plus row scales by one cubic rsq correction.  7 = default Cholesky with the round-1 kernels elsewhere: the
  * contraction (varying white noise: separate epoch-sum kernel, unpipelined
  * tiles) instead of the pipelined one and, for a correlated common process,
  * the right-looking dense update and the LDS Gauss-Jordan M_g inverse. */
