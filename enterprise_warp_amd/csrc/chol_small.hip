@@ -27,20 +27,21 @@ int launch_chol_small(int mode, int nb, const CholJob* jobs, int B, long long u0
       case 9: launch_chol_mfma<8, 1, 2, 3>(jobs, B, u0, n, b_off, theta, ldth, units, st); return 0;  // unblocked DPP panel (ALG 3)
       case 10: launch_chol_mfma<8, 1, 2, 5>(jobs, B, u0, n, b_off, theta, ldth, units, st); return 0;  // blocked panel, rcp / rsqrt + 2 Newton
       case 11: launch_chol_mfma<8, 1, 2, 6>(jobs, B, u0, n, b_off, theta, ldth, units, st); return 0;  // + row scales by rsqrt_fast (spills)
+      case 12: launch_chol_mfma<8, 1, 2, 7>(jobs, B, u0, n, b_off, theta, ldth, units, st); return 0;  // default without the packed row scales
       default: break;
     }
   }
   if (mode == 1) return 1;
   // default: LDL^T panel; up to NB = 8 the steps are unrolled and the panel is
-  // blocked (ALG 7: diagonal block by VALU with u_i by DPP row broadcast, the
-  // rest of the block row by MFMA with L^-1; quotients and row scales by one
-  // cubic correction of the rcp estimate); mode 2:
+  // blocked (ALG 8: diagonal block by VALU with u_i by DPP row broadcast, the
+  // rest of the block row by MFMA with L^-1; quotients by one cubic correction
+  // of the rcp estimate; phase-3 row scales packed); mode 2:
   // the round-1 Cholesky panel (looped) as the A/B baseline
   const bool base = mode == 2;
 #define EWH_CHOL_CASE(NBV)                                                                                   \
   case NBV:                                                                                                  \
     if (base) launch_chol_mfma<NBV, 0, default_waves(NBV), 0>(jobs, B, u0, n, b_off, theta, ldth, units, st); \
-    else launch_chol_mfma<NBV, (NBV <= 8), default_waves(NBV), (NBV <= 8 ? 7 : 1)>(jobs, B, u0, n, b_off, theta, ldth, units, st); \
+    else launch_chol_mfma<NBV, (NBV <= 8), default_waves(NBV), (NBV <= 8 ? 8 : 1)>(jobs, B, u0, n, b_off, theta, ldth, units, st); \
     return 0;
   switch (nb) {
     EWH_CHOL_CASE(1)

@@ -752,6 +752,25 @@ __device__ __forceinline__ void panel_ldl_row(BBt BBc, Blk&& blk, int q, int c, 
   // rows of the block row -> U = d^-1/2 V, d of row q + 4r read from the
   // diagonal (lane 17q + 4r); log-det and positivity from one lane per row
   // (c == 0); the r row (last block, row 15) is left as it is
+  if constexpr (ALG == 8 && bb >= Split<NB, ALG>::H) {
+    // (phase 3 only: in phase 1 the extra temporaries spill)
+    // packed: lane (q, c) takes d of row q + 4 (c/4) -- held in register c/4
+    // of lane (q, q + 4 (c/4)), whose own c/4 is the same -- so one gather,
+    // one rsqrt and one log-det term (lanes c % 4 == 0) cover all 16 rows;
+    // register r then takes its rows' scale from lane (q, 4r) by DPP
+    const int cr = c >> 2;
+    const double own = cr == 0 ? blk(BBc)[0] : cr == 1 ? blk(BBc)[1] : cr == 2 ? blk(BBc)[2] : blk(BBc)[3];
+    double dv = __shfl(own, 17 * q + 4 * cr);
+    if constexpr (bb == NB - 1) dv = (q == 3 && cr == 3) ? 1.0 : dv;
+    ok = ok && (dv > 0.0);
+    if ((c & 3) == 0) ldet.add(dv);
+    const double rsp = rsqrt_nr(dv);
+    static_for<0, 4>([&](auto R) {
+      constexpr int r = decltype(R)::value;
+      const double rs = row_newbcast<4 * r>(rsp);
+      static_for<bb, NB>([&](auto JJ) { blk(JJ)[r] *= rs; });
+    });
+  } else
   static_for<0, 4>([&](auto R) {
     constexpr int r = decltype(R)::value;
     const bool rrow = (bb == NB - 1 && r == 3) && q == 3;

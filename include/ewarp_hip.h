@@ -204,7 +204,9 @@ double ewh_unit_cost(const ewh_handle* h, int32_t pulsar);
  * update exec-masked, 9 = unblocked DPP panel (every block of the row by
  * VALU), 10 = blocked panel with the quotients by two Newton steps on the
  * hardware rcp estimate (the default uses one cubic correction), 11 = the
- * default plus row scales by one cubic rsq correction.  7 = default Cholesky with the round-1 kernels elsewhere: the
+ * default plus row scales by one cubic rsq correction, 12 = the default
+ * without the packed phase-3 row scales (four gathers + rsqrts per block row
+ * instead of one).  7 = default Cholesky with the round-1 kernels elsewhere: the
  * contraction (varying white noise: separate epoch-sum kernel, unpipelined
  * tiles) instead of the pipelined one and, for a correlated common process,
  * the right-looking dense update and the LDS Gauss-Jordan M_g inverse. */
