@@ -552,6 +552,10 @@ __device__ __forceinline__ void syrk_update(v4d& C, const v4d& Ui, const v4d& Uj
 // (one vector rsqrt per register instead of one serial rsqrt per pivot).  The
 // per-pivot dependency chain drops the scale -> ds_bpermute leg; log|Sigma| =
 // sum log d_k is accumulated per block row from the lanes' own pivots.
+// ALG 5-8 are the blocked panel (diagonal block by VALU, the rest of the row
+// by MFMA with E = L^-T); 6-8 form the pivot quotients by div_fast (one cubic
+// correction), 6 also the row scales by rsqrt_fast (spills), 8 (default)
+// packs the phase-3 row scales into one gather + one rsqrt per block row.
 // LDL^T panel of block row BB over the blocks blk(j), j = BB..NB-1 (C/D
 // layout, upper triangle), used by the register-resident kernels: the 16
 // pivots are factored by VALU (ALG 1: row k broadcast by ds_bpermute, ALG 2:
