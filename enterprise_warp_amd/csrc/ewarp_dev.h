@@ -515,7 +515,7 @@ struct Split {
   // (phase 1's 21 blocks + panel temporaries then fit 256 VGPRs without
   // spills; phase 2 runs row by row).  The blocked panel (ALG 5) has fewer
   // panel temporaries and fits at NB/2 = 4 with no scratch (3 spills).
-  static constexpr int H = (NB == 8 && ALG < 5) ? 3 : NB / 2;
+  static constexpr int H = (NB == 8 && (ALG < 5 || ALG == 9)) ? 3 : NB / 2;
   static constexpr int M = NB - H;                    // A22 block order
   static constexpr int n1 = H * NB - H * (H - 1) / 2; // blocks (i < H, j >= i)
   static constexpr int n2 = M * (M + 1) / 2;          // blocks (H <= i <= j)
@@ -756,7 +756,7 @@ __device__ __forceinline__ void panel_ldl_row(BBt BBc, Blk&& blk, int q, int c, 
   // rows of the block row -> U = d^-1/2 V, d of row q + 4r read from the
   // diagonal (lane 17q + 4r); log-det and positivity from one lane per row
   // (c == 0); the r row (last block, row 15) is left as it is
-  if constexpr (ALG == 8 && bb >= Split<NB, ALG>::H) {
+  if constexpr ((ALG == 8 && bb >= Split<NB, ALG>::H) || ALG == 9) {
     // (phase 3 only: in phase 1 the extra temporaries spill)
     // packed: lane (q, c) takes d of row q + 4 (c/4) -- held in register c/4
     // of lane (q, q + 4 (c/4)), whose own c/4 is the same -- so one gather,

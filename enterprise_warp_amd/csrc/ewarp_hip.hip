@@ -1350,7 +1350,7 @@ int ewh_create(const ewh_pta_desc* d, int device, ewh_handle** out) {
 }
 
 int ewh_set_kernel_mode(ewh_handle* h, int32_t mode) {
-  if (!h || mode < 0 || mode > 12) return set_err(EWH_E_INVALID, "bad handle / mode");
+  if (!h || mode < 0 || mode > 13) return set_err(EWH_E_INVALID, "bad handle / mode");
   h->kernel_mode = mode;
   return 0;
 }

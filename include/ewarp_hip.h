@@ -206,7 +206,8 @@ double ewh_unit_cost(const ewh_handle* h, int32_t pulsar);
  * hardware rcp estimate (the default uses one cubic correction), 11 = the
  * default plus row scales by one cubic rsq correction, 12 = the default
  * without the packed phase-3 row scales (four gathers + rsqrts per block row
- * instead of one).  7 = default Cholesky with the round-1 kernels elsewhere: the
+ * instead of one), 13 = phase split H = 3 with every row scale packed.
+ * 7 = default Cholesky with the round-1 kernels elsewhere: the
  * contraction (varying white noise: separate epoch-sum kernel, unpipelined
  * tiles) instead of the pipelined one and, for a correlated common process,
  * the right-looking dense update and the LDS Gauss-Jordan M_g inverse. */

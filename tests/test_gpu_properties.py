@@ -63,7 +63,7 @@ def test_c3_pulsar_permutation_invariance(require_gpu, c3):
     assert np.all(np.abs(a - b) <= lnl_tolerance(a))
 
 
-@pytest.mark.parametrize("mode", [0, 2, 3, 4, 5, 6, 8, 9, 10, 11, 12])
+@pytest.mark.parametrize("mode", [0, 2, 3, 4, 5, 6, 8, 9, 10, 11, 12, 13])
 def test_c3_chol_variants_vs_oracle(require_gpu, c3, mode):
     """Every register-blocked Cholesky variant (Cholesky / LDL^T panel, looped
     / unrolled, 1-2 waves per SIMD) against the oracle on full-size C3: near-
