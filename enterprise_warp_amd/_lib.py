@@ -2,15 +2,18 @@
 
 The library is built in-tree (`enterprise_warp_amd/libewarp_hip.so`, see
 csrc/Makefile / __graft_entry__.build).  There is no CPU fallback: if the
-library or a GPU is missing, the likelihood raises.
+library or a GPU is missing, the likelihood raises.  EWARP_HIP_LIB selects
+another build of the same ABI (the dev library libewarp_hip_dev.so with the
+kernel A/B variants and diagnostic exports: scripts/chol_ab.py, gpu_ab tests).
 """
 import ctypes as C
 import os
 
 _HERE = os.path.dirname(os.path.abspath(__file__))
-LIB_PATH = os.path.join(_HERE, "libewarp_hip.so")
+LIB_PATH = os.environ.get("EWARP_HIP_LIB") or os.path.join(_HERE, "libewarp_hip.so")
+DEV_LIB_PATH = os.path.join(_HERE, "libewarp_hip_dev.so")
 
-EWH_ABI_VERSION = 4
+EWH_ABI_VERSION = 5
 COMMON_CORRELATED, COMMON_OPTSTAT = 0, 1
 SPEC_POWERLAW, SPEC_TURNOVER, SPEC_FREESPEC, SPEC_CONST = 1, 2, 3, 4
 
@@ -48,8 +51,10 @@ class PtaDesc(C.Structure):
                 ("white_fixed", C.c_int32), ("pulsars", C.POINTER(PulsarDesc)), ("common", C.POINTER(CommonDesc))]
 
 
-EXPORTS = ["ewh_create", "ewh_lnl_batch", "ewh_lnl_units_device", "ewh_last_unit_terms", "ewh_unit_cost",
-           "ewh_set_kernel_mode", "ewh_optstat", "ewh_destroy", "ewh_last_error", "ewh_version"]
+EXPORTS = ["ewh_create", "ewh_num_devices", "ewh_set_fixed_white", "ewh_lnl_batch", "ewh_lnl_units_device",
+           "ewh_last_unit_terms", "ewh_unit_cost", "ewh_set_kernel_mode", "ewh_optstat", "ewh_destroy",
+           "ewh_last_error", "ewh_version"]
+DEV_EXPORTS = ["ewh_dev_gram", "ewh_dev_reduced"]
 
 _lib = None
 
@@ -75,8 +80,12 @@ def load():
         raise EngineError(f"{LIB_PATH} not built: run `make -C enterprise_warp_amd/csrc` or "
                           "__graft_entry__.build(); there is no CPU fallback")
     lib = C.CDLL(LIB_PATH)
-    lib.ewh_create.argtypes = [C.POINTER(PtaDesc), C.c_int, C.POINTER(C.c_void_p)]
+    lib.ewh_create.argtypes = [C.POINTER(PtaDesc), _ip, C.c_int32, C.POINTER(C.c_void_p)]
     lib.ewh_create.restype = C.c_int
+    lib.ewh_num_devices.argtypes = [C.c_void_p]
+    lib.ewh_num_devices.restype = C.c_int
+    lib.ewh_set_fixed_white.argtypes = [C.c_void_p, _dp]
+    lib.ewh_set_fixed_white.restype = C.c_int
     lib.ewh_lnl_batch.argtypes = [C.c_void_p, _dp, C.c_int32, _dp]
     lib.ewh_lnl_batch.restype = C.c_int
     lib.ewh_lnl_units_device.argtypes = [C.c_void_p, C.c_void_p, C.c_int32, C.c_int64, C.c_int64, C.c_void_p,
@@ -96,6 +105,11 @@ def load():
     lib.ewh_last_error.restype = C.c_char_p
     lib.ewh_version.argtypes = []
     lib.ewh_version.restype = C.c_int
+    if hasattr(lib, "ewh_dev_gram"):
+        lib.ewh_dev_gram.argtypes = [C.c_void_p, C.c_int32, _dp, C.c_int32, _dp]
+        lib.ewh_dev_gram.restype = C.c_int
+        lib.ewh_dev_reduced.argtypes = [C.c_void_p, C.c_int32, _dp, _dp]
+        lib.ewh_dev_reduced.restype = C.c_int
     if lib.ewh_version() != EWH_ABI_VERSION:
         raise EngineError("libewarp_hip.so ABI version mismatch")
     _lib = lib

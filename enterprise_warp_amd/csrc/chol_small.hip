@@ -1,5 +1,6 @@
 // chol_small.hip — register-resident factorisation chol_mfma_kernel<NB <= 9>
-// and its A/B variants (see ewarp_dev.h, ewh_set_kernel_mode).
+// and (dev library only, -DEWH_DEV) its A/B variants (see ewarp_dev.h,
+// ewh_set_kernel_mode).
 #include "ewarp_dev.h"
 
 namespace ewh_dev {
@@ -14,8 +15,15 @@ void launch_chol_mfma(const CholJob* jobs, int B, long long u0, long long n, int
 
 }  // namespace
 
+#ifdef EWH_DEV
+bool ab_variants_built() { return true; }
+#else
+bool ab_variants_built() { return false; }
+#endif
+
 int launch_chol_small(int mode, int nb, const CholJob* jobs, int B, long long u0, long long n, int b_off,
                       const double* theta, int ldth, double* units, hipStream_t st) {
+#ifdef EWH_DEV
   // A/B variants (NB = 8, the C3 reduced width)
   if (nb == 8 && mode >= 3) {
     switch (mode) {
@@ -32,6 +40,7 @@ int launch_chol_small(int mode, int nb, const CholJob* jobs, int B, long long u0
       default: break;
     }
   }
+#endif
   if (mode == 1) return 1;
   // default: LDL^T panel; up to NB = 8 the steps are unrolled and the panel is
   // blocked (ALG 8: diagonal block by VALU with u_i by DPP row broadcast, the

@@ -28,7 +28,10 @@ int dispatch_contract(int nb, const PsrDev& P, const double* w, const double* be
     case 11: launch_contract<11>(P, w, beta, s, fac, G, nb_samples, st); break;
     case 12: launch_contract<12>(P, w, beta, s, fac, G, nb_samples, st); break;
     case 13: launch_contract<13>(P, w, beta, s, fac, G, nb_samples, st); break;
-    default: return set_err(EWH_E_UNSUPPORTED, "basis too wide for the contraction kernel (> 207 columns)");
+    case 14: launch_contract<14>(P, w, beta, s, fac, G, nb_samples, st); break;
+    case 15: launch_contract<15>(P, w, beta, s, fac, G, nb_samples, st); break;
+    case 16: launch_contract<16>(P, w, beta, s, fac, G, nb_samples, st); break;
+    default: return set_err(EWH_E_UNSUPPORTED, "basis too wide for the contraction kernel (> 255 columns)");
   }
   return 0;
 }
@@ -37,12 +40,7 @@ template <int NB>
 int launch_contract2(const PsrDev& P, const double* w, const double* beta, double* s, long long s_stride, double* G,
                      int nb_samples, hipStream_t st) {
   const size_t lds = (size_t)(2 * CT_ROWS * 16 * NB + 3 * CT_ROWS) * sizeof(double);
-  static bool attr = false;
-  if (!attr) {
-    EWH_HIP(hipFuncSetAttribute((const void*)contract2_kernel<NB>, hipFuncAttributeMaxDynamicSharedMemorySize,
-                                (int)lds));
-    attr = true;
-  }
+  // (the dynamic-LDS attribute is set per device by set_contract_attributes)
   hipLaunchKernelGGL(HIP_KERNEL_NAME(contract2_kernel<NB>), dim3(nb_samples), dim3(256), lds, st, P, w, beta, s,
                      s_stride, G);
   return 0;
@@ -64,11 +62,38 @@ int dispatch_contract2(int nb, const PsrDev& P, const double* w, const double* b
     case 11: return launch_contract2<11>(P, w, beta, s, s_stride, G, nb_samples, st);
     case 12: return launch_contract2<12>(P, w, beta, s, s_stride, G, nb_samples, st);
     case 13: return launch_contract2<13>(P, w, beta, s, s_stride, G, nb_samples, st);
-    default: return set_err(EWH_E_UNSUPPORTED, "basis too wide for the contraction kernel (> 207 columns)");
+    default: return set_err(EWH_E_UNSUPPORTED, "basis too wide for the pipelined contraction (> 207 columns)");
   }
 }
 
+template <int NB>
+int set_attr2() {
+  const size_t lds = (size_t)(2 * CT_ROWS * 16 * NB + 3 * CT_ROWS) * sizeof(double);
+  EWH_HIP(hipFuncSetAttribute((const void*)contract2_kernel<NB>, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds));
+  return 0;
+}
+
+template <int NB>
+int set_attr1() {
+  const size_t lds = (size_t)(CT_ROWS * 16 * NB + CT_ROWS) * sizeof(double);
+  EWH_HIP(hipFuncSetAttribute((const void*)contract_mfma_kernel<NB>, hipFuncAttributeMaxDynamicSharedMemorySize,
+                              (int)lds));
+  return 0;
+}
+
 }  // namespace
+
+// dynamic-LDS limits of every contraction instantiation on the current device
+int set_contract_attributes() {
+  int rc = 0;
+  static_for<1, CONTRACT2_NB_MAX + 1>([&](auto N) {
+    if (!rc) rc = set_attr2<decltype(N)::value>();
+  });
+  static_for<1, 17>([&](auto N) {
+    if (!rc) rc = set_attr1<decltype(N)::value>();
+  });
+  return rc;
+}
 
 int launch_contract_nb(int nb, const PsrDev& P, const double* w, const double* beta, const double* s,
                        const double* fac, double* G, int nb_samples, hipStream_t st) {

@@ -40,6 +40,15 @@ typedef double v4d __attribute__((ext_vector_type(4)));
 // ----------------------------------------------------------------------------
 // device helpers
 // ----------------------------------------------------------------------------
+// compile-time loop: f(std::integral_constant<int, I>) for I in [B, E)
+template <int B, int E, typename F>
+__host__ __device__ __forceinline__ void static_for(F&& f) {
+  if constexpr (B < E) {
+    f(std::integral_constant<int, B>{});
+    static_for<B + 1, E>(f);
+  }
+}
+
 __device__ __forceinline__ double pref_val(const ewh_pref& r, const double* th) {
   return r.idx >= 0 ? th[r.idx] : r.cval;
 }
@@ -454,6 +463,13 @@ __device__ __forceinline__ void contract2_body(const PsrDev& P, const double* __
       }
       __syncthreads();                               // drains the glds of tile it+1 (vmcnt(0))
     }
+    if (pass == 0 && ecorr && tid < LD) {
+      // pad rows [n_epoch, whole tiles) of the epoch pass: zero, so a value a
+      // previous pulsar / sample left in the shared scratch never meets the
+      // zero weight of the pad rows (0 * inf = NaN)
+      const int epad = ((P.n_epoch + CT_ROWS - 1) / CT_ROWS) * CT_ROWS;
+      for (int e = P.n_epoch; e < epad; ++e) srow[(long long)e * LD + tid] = 0.0;
+    }
     if (pass == 0 && ecorr) __threadfence_block();   // s_e rows visible to the epoch pass
     __syncthreads();
   }
@@ -523,14 +539,6 @@ struct Split {
   static constexpr int i2(int i, int j) { return (i - H) * M - ((i - H) * (i - H - 1)) / 2 + (j - i); }
 };
 
-// compile-time loop: f(std::integral_constant<int, I>) for I in [B, E)
-template <int B, int E, typename F>
-__device__ __forceinline__ void static_for(F&& f) {
-  if constexpr (B < E) {
-    f(std::integral_constant<int, B>{});
-    static_for<B + 1, E>(f);
-  }
-}
 
 // A -= U_i^T U_j : four f64 MFMAs.  For the f64 MFMAs of gfx940+ the last
 // (blgp) field is the neg modifier (bit 0 negates A: `neg:[1,0,0]`), so no
@@ -1113,5 +1121,9 @@ int launch_chol_big_nb(int nb, const CholJob* jobs, int B, long long u0, long lo
                        const double* theta, int ldth, double* units, double* scr, long long cap, hipStream_t st);
 int launch_partial_nb(int nb, int keep, const CholJob* jobs, int B, long long u0, long long n,
                       const double* theta, int ldth, double* units, double* keep_out, int P, hipStream_t st);
+// dynamic-LDS attributes of the contraction kernels on the current device
+int set_contract_attributes();
+// true in the dev library (make dev, -DEWH_DEV): kernel A/B modes 3-6, 8-13 compiled in
+bool ab_variants_built();
 
 }  // namespace ewh_dev

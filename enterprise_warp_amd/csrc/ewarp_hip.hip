@@ -229,7 +229,6 @@ __global__ __launch_bounds__(256) void common_minv_kernel(const CommonPsr* __res
   double* colk = sm + P * LDP;
   double* rowk = colk + P;
   double* own = rowk + P;
-  __shared__ double red[4];
   const int slot = blockIdx.x, g = uniq[slot], bl = blockIdx.y;
   const double* th = theta + (long long)(b0 + bl) * ldth;
   const double pc = spec_phi(cspec[g], th);
@@ -748,11 +747,14 @@ struct PsrHost {
   DSpec* d_fx_spec = nullptr;
   double* d_S = nullptr;          // fx_ld^2
   bool has_theta_white = false;
+  int n_slot = 0;
+  ewh_pref* d_slots = nullptr;    // device copy of the white-noise slot table (PsrDev::slots)
+  std::vector<ewh_pref> slots;    // host copy (ewh_set_fixed_white updates the constants)
 };
 
 }  // namespace
 
-struct ewh_handle {
+struct DevCtx {
   int device = 0;
   int P = 0, n_param = 0;
   bool white_fixed = false;
@@ -777,6 +779,7 @@ struct ewh_handle {
   long long bigscr_cap = 0;   // workgroups per launch it holds
   int bigscr_nb = 0;
   int chunk = 0;
+  int chunk_cap = 0;          // largest chunk the ~1.5 GB scratch budget allows
   int last_B = 0;
   // correlated common process (fixed white noise)
   bool corr = false;
@@ -791,13 +794,15 @@ struct ewh_handle {
   double *d_cldet = nullptr, *d_cq = nullptr;
   int* d_cfail = nullptr;
   size_t keep_cap = 0;
+  int cchunk_cap = 0;         // samples the dense Sigma_c budget allows per chunk
+  int n_param_desc = 0;
   bool osmode = false;        // EWH_COMMON_OPTSTAT handle (ewh_optstat only)
 };
 
 namespace {
 
 template <typename T>
-int dalloc(ewh_handle* h, T** p, size_t count) {
+int dalloc(DevCtx* h, T** p, size_t count) {
   *p = nullptr;
   if (count == 0) count = 1;
   hipError_t e = hipMalloc((void**)p, count * sizeof(T));
@@ -807,7 +812,7 @@ int dalloc(ewh_handle* h, T** p, size_t count) {
 }
 
 template <typename T>
-int dupload(ewh_handle* h, T** p, const T* src, size_t count) {
+int dupload(DevCtx* h, T** p, const T* src, size_t count) {
   int rc = dalloc(h, p, count);
   if (rc) return rc;
   if (count) EWH_HIP(hipMemcpy(*p, src, count * sizeof(T), hipMemcpyHostToDevice));
@@ -949,22 +954,17 @@ int dispatch_chol(int mode, int nb, int mreal, const CholJob* jobs, int B, long 
   }
   const size_t lds = lds_bytes_chol(mreal);
   if (lds > LDS_MAX - 64) return set_err(EWH_E_UNSUPPORTED, "reduced matrix too large for the LDS Cholesky kernel");
-  static bool attr_set = false;
-  if (!attr_set) {
-    EWH_HIP(hipFuncSetAttribute((const void*)chol_lds_kernel, hipFuncAttributeMaxDynamicSharedMemorySize,
-                                (int)(LDS_MAX - 64)));
-    attr_set = true;
-  }
+  // (the dynamic-LDS attribute of chol_lds_kernel is set per device in create_ctx)
   hipLaunchKernelGGL(chol_lds_kernel, dim3((unsigned)n), dim3(256), lds, st, jobs, B, u0, b_off, theta, ldth, units);
   return 0;
 }
 
 // scratch of chol_big_kernel for NB: BIG_SLOTS workgroups x NB(NB+1)/2 blocks of 2 KiB
 constexpr long long BIG_SLOTS = 2048;
-int ensure_big_scratch(ewh_handle* h, int nb) {
+int ensure_big_scratch(DevCtx* h, int nb) {
   if (nb <= MFMA_NB_MAX || nb > BIG_NB_MAX || nb <= h->bigscr_nb) return 0;
   if (h->d_bigscr) {
-    hipFree(h->d_bigscr);
+    (void)hipFree(h->d_bigscr);
     h->allocs.erase(std::find(h->allocs.begin(), h->allocs.end(), (void*)h->d_bigscr));
     h->d_bigscr = nullptr;
   }
@@ -975,11 +975,11 @@ int ensure_big_scratch(ewh_handle* h, int nb) {
   return 0;
 }
 
-int ensure_units(ewh_handle* h, int B) {
+int ensure_units(DevCtx* h, int B) {
   const size_t need = (size_t)(h->P + (h->corr ? 1 : 0)) * B;   // + the common term row
   if (need <= h->units_cap) return 0;
   if (h->d_units) {
-    hipFree(h->d_units);
+    (void)hipFree(h->d_units);
     h->allocs.erase(std::find(h->allocs.begin(), h->allocs.end(), (void*)h->d_units));
   }
   h->units_cap = 0;
@@ -989,12 +989,14 @@ int ensure_units(ewh_handle* h, int B) {
   return 0;
 }
 
-int ensure_var_scratch(ewh_handle* h, int B) {
+int ensure_var_scratch(DevCtx* h, int B) {
   if (h->white_fixed) return 0;
-  if (h->chunk > 0 && (h->chunk >= B || h->chunk >= 1024)) return 0;
+  // reuse while the chunk covers the batch or already sits at its cap (the
+  // memory-derived limit, at most 1024): no free / re-malloc per call
+  if (h->chunk > 0 && (h->chunk >= B || h->chunk >= h->chunk_cap)) return 0;
   for (void* p : {(void*)h->d_w, (void*)h->d_beta, (void*)h->d_s, (void*)h->d_G, (void*)h->d_Kb, (void*)h->d_fac}) {
     if (p) {
-      hipFree(p);
+      (void)hipFree(p);
       h->allocs.erase(std::find(h->allocs.begin(), h->allocs.end(), p));
     }
   }
@@ -1010,8 +1012,9 @@ int ensure_var_scratch(ewh_handle* h, int B) {
   // contraction's last epoch tile reads zero-initialised pad rows
   const size_t sstride = ((maxe + CT_ROWS - 1) / CT_ROWS + 1) * CT_ROWS * maxld;
   const size_t per = (maxld * maxld + sstride + maxn + maxe + maxfac + 1) * sizeof(double);
-  size_t chunk = std::max<size_t>(1, (size_t)1536 * 1024 * 1024 / per);
-  chunk = std::min<size_t>(chunk, std::min<size_t>(std::max(B, 1), 1024));
+  const size_t cap = std::min<size_t>(1024, std::max<size_t>(1, (size_t)1536 * 1024 * 1024 / per));
+  h->chunk_cap = (int)cap;
+  const size_t chunk = std::min<size_t>(cap, (size_t)std::max(B, 1));
   int rc;
   if ((rc = dalloc(h, &h->d_w, chunk * maxn))) return rc;
   if ((rc = dalloc(h, &h->d_beta, chunk * maxe))) return rc;
@@ -1032,7 +1035,7 @@ int ensure_var_scratch(ewh_handle* h, int B) {
 }
 
 // white-noise terms of one pulsar for samples [b0, b0 + nb) into the chunk scratch
-int run_white(ewh_handle* h, int p, const double* theta, int ldth, int b0, int nb) {
+int run_white(DevCtx* h, int p, const double* theta, int ldth, int b0, int nb) {
   PsrHost& ps = h->psr[p];
   hipLaunchKernelGGL(wn_weights_kernel, dim3(nb), dim3(256), 0, h->stream, ps.dev, theta, ldth, b0, h->d_w,
                      h->d_beta, h->d_Kb, h->d_fac);
@@ -1051,8 +1054,27 @@ int run_white(ewh_handle* h, int p, const double* theta, int ldth, int b0, int n
   return 0;
 }
 
-int setup_fixed(ewh_handle* h, const ewh_pta_desc* d) {
-  // one-sample scratch; theta is never read (all white-noise slots constant)
+// Temporary device buffers of a one-off setup step (freed on scope exit).
+struct TmpBufs {
+  std::vector<void*> p;
+  template <typename T>
+  int get(T** out, size_t count) {
+    *out = nullptr;
+    hipError_t e = hipMalloc((void**)out, std::max<size_t>(1, count) * sizeof(T));
+    if (e != hipSuccess) return set_err(EWH_E_NOMEM, std::string("hipMalloc: ") + hipGetErrorString(e));
+    p.push_back(*out);
+    return 0;
+  }
+  ~TmpBufs() {
+    for (void* q : p) (void)hipFree(q);
+  }
+};
+
+// Fixed white noise: G = T_aug^T N^-1 T_aug of every pulsar at the constant
+// white-noise values, then the timing-model elimination (schur_kernel) into
+// the cached reduced matrix S_p and constant K_p.  Called by create and again
+// by ewh_set_fixed_white (new constants, same layout: buffers are reused).
+int setup_fixed(DevCtx* h) {
   int rc;
   size_t maxn = 1, maxe = 1, maxld = 16;
   for (auto& ps : h->psr) {
@@ -1060,18 +1082,18 @@ int setup_fixed(ewh_handle* h, const ewh_pta_desc* d) {
     maxe = std::max(maxe, (size_t)ps.n_epoch);
     maxld = std::max(maxld, (size_t)ps.ld);
   }
-  double *w, *beta, *s, *G, *Kb;
-  if ((rc = dalloc(h, &w, maxn))) return rc;
-  if ((rc = dalloc(h, &beta, maxe))) return rc;
-  if ((rc = dalloc(h, &s, maxe * maxld))) return rc;
-  if ((rc = dalloc(h, &G, maxld * maxld))) return rc;
-  if ((rc = dalloc(h, &Kb, 1))) return rc;
-  double* dummy_theta;
-  if ((rc = dalloc(h, &dummy_theta, std::max(1, d->n_param)))) return rc;
-  EWH_HIP(hipMemset(dummy_theta, 0, sizeof(double) * std::max(1, d->n_param)));
-  if ((rc = dalloc(h, &h->d_fxK, h->P))) return rc;
-  if ((rc = dalloc(h, &h->d_fxfail, h->P))) return rc;
+  TmpBufs tmp;
+  double *w, *beta, *s, *G, *Kb, *dummy_theta;
+  if ((rc = tmp.get(&w, maxn)) || (rc = tmp.get(&beta, maxe)) || (rc = tmp.get(&s, maxe * maxld)) ||
+      (rc = tmp.get(&G, maxld * maxld)) || (rc = tmp.get(&Kb, 1)) ||
+      (rc = tmp.get(&dummy_theta, std::max(1, h->n_param))))
+    return rc;
+  // theta is never read (every white-noise slot is constant)
+  EWH_HIP(hipMemsetAsync(dummy_theta, 0, sizeof(double) * std::max(1, h->n_param), h->stream));
+  if (!h->d_fxK && (rc = dalloc(h, &h->d_fxK, h->P))) return rc;
+  if (!h->d_fxfail && (rc = dalloc(h, &h->d_fxfail, h->P))) return rc;
   std::vector<CholJob> jobs(h->P);
+  std::vector<int> fails(h->P, 0);
   for (int p = 0; p < h->P; ++p) {
     PsrHost& ps = h->psr[p];
     hipLaunchKernelGGL(wn_weights_kernel, dim3(1), dim3(256), 0, h->stream, ps.dev, dummy_theta, 0, 0, w, beta, Kb,
@@ -1082,25 +1104,25 @@ int setup_fixed(ewh_handle* h, const ewh_pta_desc* d) {
     double Kb_h = 0.0;
     EWH_HIP(hipMemcpyAsync(&Kb_h, Kb, sizeof(double), hipMemcpyDeviceToHost, h->stream));
     EWH_HIP(hipStreamSynchronize(h->stream));
-    if ((rc = dalloc(h, &ps.d_S, (size_t)ps.fx_ld * ps.fx_ld))) return rc;
+    if (!ps.d_S && (rc = dalloc(h, &ps.d_S, (size_t)ps.fx_ld * ps.fx_ld))) return rc;
     hipLaunchKernelGGL(schur_kernel, dim3(1), dim3(256), 0, h->stream, G, ps.ld, ps.m, ps.nlead, ps.d_colptr,
                        ps.d_spec, Kb_h, ps.d_S, ps.fx_ld, ps.nloc, ps.gstart, ps.ncommon, h->d_fxK + p,
                        h->d_fxfail + p);
     EWH_HIP(hipGetLastError());
-    EWH_HIP(hipStreamSynchronize(h->stream));
-    int fail = 0;
-    EWH_HIP(hipMemcpy(&fail, h->d_fxfail + p, sizeof(int), hipMemcpyDeviceToHost));
     // mreal: columns that take phi^-1 in the factorisation -- the own columns
     // (correlated: the common block is assembled globally), or every column
     // with entries (optimal statistic: the CURN Sigma of each pulsar)
     const int mreal = h->osmode ? ps.fx_ld - 1 : ps.nloc;
-    jobs[p] = CholJob{ps.d_S, 0, ps.fx_ld, mreal, ps.d_fx_colptr, ps.d_fx_spec, h->d_fxK + p, 0, fail};
+    jobs[p] = CholJob{ps.d_S, 0, ps.fx_ld, mreal, ps.d_fx_colptr, ps.d_fx_spec, h->d_fxK + p, 0, 0};
   }
+  EWH_HIP(hipMemcpyAsync(fails.data(), h->d_fxfail, sizeof(int) * h->P, hipMemcpyDeviceToHost, h->stream));
+  EWH_HIP(hipStreamSynchronize(h->stream));
+  for (int p = 0; p < h->P; ++p) jobs[p].fail = fails[p];
   EWH_HIP(hipMemcpy(h->d_jobs_fixed, jobs.data(), sizeof(CholJob) * h->P, hipMemcpyHostToDevice));
   return 0;
 }
 
-int setup_common(ewh_handle* h, const ewh_pta_desc* d) {
+int setup_common(DevCtx* h, const ewh_pta_desc* d) {
   const ewh_common_desc& c = *d->common;
   const int P = h->P;
   h->corr = true;
@@ -1164,29 +1186,46 @@ int setup_common(ewh_handle* h, const ewh_pta_desc* d) {
   if ((rc = dupload(h, &h->d_cps, cps.data(), cps.size()))) return rc;
   h->Np = DCB * ((P * h->nc + 1 + DCB - 1) / DCB);
   const double per = (double)h->Np * h->Np * 8.0;
-  h->cchunk = (int)std::max(1.0, std::min(1024.0, 40.0e9 / per));   // <= 40 GB of dense Sigma_c per chunk
-  const size_t Bc = h->cchunk;
-  if ((rc = dalloc(h, &h->d_minv, Bc * h->nc * P * P))) return rc;
-  if ((rc = dalloc(h, &h->d_mlog, Bc * h->nc))) return rc;
-  if ((rc = dalloc(h, &h->d_dense, Bc * h->Np * h->Np))) return rc;
-  if ((rc = dalloc(h, &h->d_wbuf, Bc * DCB * DCB))) return rc;
-  if ((rc = dalloc(h, &h->d_cldet, Bc))) return rc;
-  if ((rc = dalloc(h, &h->d_cq, Bc))) return rc;
-  if ((rc = dalloc(h, &h->d_cfail, Bc))) return rc;
+  h->cchunk_cap = (int)std::max(1.0, std::min(1024.0, 40.0e9 / per));   // <= 40 GB of dense Sigma_c per chunk
+  h->cchunk = 0;              // the chunk scratch is allocated on first use, sized to the batch
   const size_t lds = ((size_t)P * (P + 1) + 3 * P) * sizeof(double);
   EWH_HIP(hipFuncSetAttribute((const void*)common_minv_kernel, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds));
   return 0;
 }
 
+// per-chunk scratch of the dense cross-pulsar factorisation, sized to
+// min(B, cap) on first use and grown (up to the cap) when a larger batch comes
+int ensure_common_scratch(DevCtx* h, int B) {
+  const int want = std::min(std::max(B, 1), h->cchunk_cap);
+  if (h->cchunk >= want) return 0;
+  for (void* p : {(void*)h->d_minv, (void*)h->d_mlog, (void*)h->d_dense, (void*)h->d_wbuf, (void*)h->d_cldet,
+                  (void*)h->d_cq, (void*)h->d_cfail}) {
+    if (p) {
+      (void)hipFree(p);
+      h->allocs.erase(std::find(h->allocs.begin(), h->allocs.end(), p));
+    }
+  }
+  h->cchunk = 0;
+  const size_t Bc = want, P = h->P;
+  int rc;
+  if ((rc = dalloc(h, &h->d_minv, Bc * h->nc * P * P)) || (rc = dalloc(h, &h->d_mlog, Bc * h->nc)) ||
+      (rc = dalloc(h, &h->d_dense, Bc * h->Np * h->Np)) || (rc = dalloc(h, &h->d_wbuf, Bc * DCB * DCB)) ||
+      (rc = dalloc(h, &h->d_cldet, Bc)) || (rc = dalloc(h, &h->d_cq, Bc)) || (rc = dalloc(h, &h->d_cfail, Bc)))
+    return rc;
+  h->cchunk = want;
+  return 0;
+}
+
 // correlated batch: per-pulsar partial factorisations of every unit, then per
 // sample chunk the common-block assembly and the dense factorisation
-int lnl_correlated(ewh_handle* h, const double* theta_dev, int B, hipStream_t st) {
+int lnl_correlated(DevCtx* h, const double* theta_dev, int B, hipStream_t st) {
   const int P = h->P, ldth = h->n_param, KD = 16 * h->keep;
   int rc;
+  if ((rc = ensure_common_scratch(h, B))) return rc;
   const size_t need = (size_t)B * P * KD * KD;
   if (need > h->keep_cap) {
     if (h->d_keep) {
-      hipFree(h->d_keep);
+      (void)hipFree(h->d_keep);
       h->allocs.erase(std::find(h->allocs.begin(), h->allocs.end(), (void*)h->d_keep));
       h->d_keep = nullptr;
     }
@@ -1243,29 +1282,38 @@ int lnl_correlated(ewh_handle* h, const double* theta_dev, int B, hipStream_t st
 
 }  // namespace
 
-extern "C" {
+namespace {
 
-int ewh_version(void) { return EWH_ABI_VERSION; }
+void destroy_ctx(DevCtx* h) {
+  if (!h) return;
+  (void)hipSetDevice(h->device);
+  if (h->stream) (void)hipStreamSynchronize(h->stream);
+  for (void* p : h->allocs) (void)hipFree(p);
+  if (h->stream) (void)hipStreamDestroy(h->stream);
+  delete h;
+}
 
-const char* ewh_last_error(void) { return g_err.c_str(); }
-
-int ewh_create(const ewh_pta_desc* d, int device, ewh_handle** out) {
-  if (!out) return set_err(EWH_E_INVALID, "out is NULL");
+// One device's copy of the PTA (every table, the fixed-WN cache, scratch).
+int create_ctx(const ewh_pta_desc* d, int device, DevCtx** out) {
   *out = nullptr;
-  int rc = validate(d);
-  if (rc) return rc;
+  int rc;
   EWH_HIP(hipSetDevice(device));
-  ewh_handle* h = new ewh_handle();
+  DevCtx* h = new DevCtx();
   h->device = device;
   h->P = d->n_pulsar;
   h->n_param = d->n_param;
   h->psr.resize(h->P);
   auto bail = [&](int code) {
-    ewh_destroy(h);
+    destroy_ctx(h);
     return code;
   };
   if (hipStreamCreateWithFlags(&h->stream, hipStreamNonBlocking) != hipSuccess)
     return bail(set_err(EWH_E_HIP, "hipStreamCreate failed"));
+  // per device (the attribute is a property of the kernel on the current device)
+  if (hipFuncSetAttribute((const void*)chol_lds_kernel, hipFuncAttributeMaxDynamicSharedMemorySize,
+                          (int)(LDS_MAX - 64)) != hipSuccess)
+    return bail(set_err(EWH_E_HIP, "hipFuncSetAttribute(chol_lds_kernel) failed"));
+  if ((rc = set_contract_attributes())) return bail(rc);
   bool any_theta_white = false;
   for (int p = 0; p < h->P; ++p) {
     const ewh_pulsar_desc& s = d->pulsars[p];
@@ -1300,12 +1348,13 @@ int ewh_create(const ewh_pta_desc* d, int device, ewh_handle** out) {
     double* dT;
     double* dsig2;
     int *d_ef, *d_eq, *d_es, *d_ee, *d_eslot;
-    ewh_pref* d_slots;
+    ps.n_slot = s.n_slot;
+    ps.slots.assign(s.slots, s.slots + s.n_slot);
     if ((rc = dupload(h, &dT, Ta.data(), Ta.size()))) return bail(rc);
     if ((rc = dupload(h, &dsig2, sig2.data(), sig2.size()))) return bail(rc);
     if ((rc = dupload(h, &d_ef, s.efac_slot, (size_t)s.n_toa))) return bail(rc);
     if ((rc = dupload(h, &d_eq, s.equad_slot, (size_t)s.n_toa))) return bail(rc);
-    if ((rc = dupload(h, &d_slots, s.slots, (size_t)s.n_slot))) return bail(rc);
+    if ((rc = dupload(h, &ps.d_slots, s.slots, (size_t)s.n_slot))) return bail(rc);
     if ((rc = dupload(h, &d_es, s.epoch_start, (size_t)s.n_epoch))) return bail(rc);
     if ((rc = dupload(h, &d_ee, s.epoch_stop, (size_t)s.n_epoch))) return bail(rc);
     if ((rc = dupload(h, &d_eslot, s.epoch_slot, (size_t)s.n_epoch))) return bail(rc);
@@ -1324,7 +1373,7 @@ int ewh_create(const ewh_pta_desc* d, int device, ewh_handle** out) {
       if ((rc = dupload(h, &d_lnc, s.ln_chrom, (size_t)s.n_toa))) return bail(rc);
       if ((rc = dupload(h, &d_bg, s.bgroup_idx, (size_t)s.n_bgroup))) return bail(rc);
     }
-    ps.dev = PsrDev{s.n_toa, s.n_col, ps.ld, ps.nb, s.n_epoch, dT, dsig2, d_ef, d_eq, d_slots, d_es, d_ee, d_eslot,
+    ps.dev = PsrDev{s.n_toa, s.n_col, ps.ld, ps.nb, s.n_epoch, dT, dsig2, d_ef, d_eq, ps.d_slots, d_es, d_ee, d_eslot,
                     s.n_bgroup, d_cbg, d_lnc, d_bg, d_tep};
     std::vector<int> ptr;
     std::vector<DSpec> ent;
@@ -1341,36 +1390,20 @@ int ewh_create(const ewh_pta_desc* d, int device, ewh_handle** out) {
   h->osmode = d->common && d->common->kind == EWH_COMMON_OPTSTAT;
   if (d->common && !h->white_fixed)
     return bail(set_err(EWH_E_UNSUPPORTED, "correlated common process: white noise must be fixed (TNT cached)"));
-  if (h->white_fixed) {
-    if ((rc = setup_fixed(h, d))) return bail(rc);
-  }
+  if (h->white_fixed && (rc = setup_fixed(h))) return bail(rc);
   if (d->common && (rc = setup_common(h, d))) return bail(rc);
   *out = h;
   return 0;
 }
 
-int ewh_set_kernel_mode(ewh_handle* h, int32_t mode) {
-  if (!h || mode < 0 || mode > 13) return set_err(EWH_E_INVALID, "bad handle / mode");
-  h->kernel_mode = mode;
-  return 0;
-}
-
-double ewh_unit_cost(const ewh_handle* h, int32_t p) {
-  if (!h || p < 0 || p >= h->P) return 0.0;
-  const PsrHost& ps = h->psr[p];
-  if (h->white_fixed) return (double)ps.fx_ld * ps.fx_ld * ps.fx_ld / 3.0;
-  return (double)ps.n_toa * ps.ld * ps.ld + (double)ps.ld * ps.ld * ps.ld / 3.0;
-}
-
-int ewh_lnl_units_device(ewh_handle* h, const double* theta_dev, int32_t B, int64_t u_begin, int64_t u_end,
-                         double* out_dev, void* stream) {
-  if (!h || !theta_dev || !out_dev || B <= 0) return set_err(EWH_E_INVALID, "bad arguments");
-  if (h->osmode) return set_err(EWH_E_UNSUPPORTED, "an optimal-statistic handle evaluates ewh_optstat only");
+// lnL terms of units [u_begin, u_end) (u = pulsar * B + sample) into h->d_units
+// (rows outside the range zeroed); reduce: also out_dev[b] = sum over the rows.
+int ctx_units(DevCtx* h, const double* theta_dev, int B, int64_t u_begin, int64_t u_end, double* out_dev,
+              hipStream_t st, bool reduce) {
   const long long U = (long long)h->P * B;
   u_begin = std::max<int64_t>(0, u_begin);
   u_end = std::min<int64_t>(U, u_end);
   EWH_HIP(hipSetDevice(h->device));
-  hipStream_t st = (hipStream_t)stream;   // NULL = the default stream, as documented
   int rc;
   if ((rc = ensure_units(h, B))) return rc;
   const int rows = h->P + (h->corr ? 1 : 0);
@@ -1378,15 +1411,15 @@ int ewh_lnl_units_device(ewh_handle* h, const double* theta_dev, int32_t B, int6
   const int ldth = h->n_param;
   hipStream_t saved = h->stream;
   h->stream = st;
+  struct Restore {
+    DevCtx* h;
+    hipStream_t s;
+    ~Restore() { h->stream = s; }
+  } restore{h, saved};
   if (h->corr) {
-    if (u_begin != 0 || u_end != U) {
-      h->stream = saved;
+    if (u_begin != 0 || u_end != U)
       return set_err(EWH_E_UNSUPPORTED, "correlated common process: pass the whole batch (shard samples, not units)");
-    }
-    if ((rc = lnl_correlated(h, theta_dev, B, st))) {
-      h->stream = saved;
-      return rc;
-    }
+    if ((rc = lnl_correlated(h, theta_dev, B, st))) return rc;
   } else if (h->white_fixed) {
     // one launch per run of consecutive pulsars with the same kernel class
     long long u = u_begin;
@@ -1400,55 +1433,42 @@ int ewh_lnl_units_device(ewh_handle* h, const double* theta_dev, int32_t B, int6
       for (int p = p0; p < p1; ++p) maxm = std::max(maxm, h->psr[p].fx_m);
       if ((rc = ensure_big_scratch(h, nb0)) ||
           (rc = dispatch_chol(h->kernel_mode, nb0, maxm, h->d_jobs_fixed, B, u, seg_end - u, 0, theta_dev, ldth,
-                              h->d_units, st, h->d_bigscr, h->bigscr_cap))) {
-        h->stream = saved;
+                              h->d_units, st, h->d_bigscr, h->bigscr_cap)))
         return rc;
-      }
       u = seg_end;
     }
   } else {
-    if ((rc = ensure_var_scratch(h, B))) {
-      h->stream = saved;
-      return rc;
-    }
+    if ((rc = ensure_var_scratch(h, B))) return rc;
     for (long long u = u_begin; u < u_end;) {
       const int p = (int)(u / B);
       const long long pend = std::min<long long>(u_end, (long long)(p + 1) * B);
       const int bs = (int)(u - (long long)p * B), be = (int)(pend - (long long)p * B);
       for (int c0 = bs; c0 < be; c0 += h->chunk) {
         const int nb = std::min(h->chunk, be - c0);
-        if ((rc = run_white(h, p, theta_dev, ldth, c0, nb))) {
-          h->stream = saved;
-          return rc;
-        }
+        if ((rc = run_white(h, p, theta_dev, ldth, c0, nb))) return rc;
         if ((rc = ensure_big_scratch(h, h->psr[p].nb)) ||
-            (rc = dispatch_chol(h->kernel_mode, h->psr[p].nb, h->psr[p].m, h->d_jobs_var, B,
-                                (long long)p * B + c0, nb, c0, theta_dev, ldth, h->d_units, st, h->d_bigscr,
-                                h->bigscr_cap))) {
-          h->stream = saved;
+            (rc = dispatch_chol(h->kernel_mode, h->psr[p].nb, h->psr[p].m, h->d_jobs_var, B, (long long)p * B + c0, nb,
+                                c0, theta_dev, ldth, h->d_units, st, h->d_bigscr, h->bigscr_cap)))
           return rc;
-        }
       }
       u = pend;
     }
   }
-  h->stream = saved;
-  hipLaunchKernelGGL(reduce_units_kernel, dim3((B + 255) / 256), dim3(256), 0, st, h->d_units, rows, B, out_dev);
+  if (reduce)
+    hipLaunchKernelGGL(reduce_units_kernel, dim3((B + 255) / 256), dim3(256), 0, st, h->d_units, rows, B, out_dev);
   EWH_HIP(hipGetLastError());
   h->last_B = B;
   return 0;
 }
 
-int ewh_lnl_batch(ewh_handle* h, const double* theta_host, int32_t B, double* out_host) {
-  if (!h || !theta_host || !out_host || B <= 0) return set_err(EWH_E_INVALID, "bad arguments");
-  EWH_HIP(hipSetDevice(h->device));
+// device theta / out buffers of one context, grown as needed
+int ensure_io(DevCtx* h, int B) {
   const size_t need = (size_t)B * std::max(1, h->n_param) + B;
   if (need > h->io_cap) {
-    for (void* p : {(void*)h->d_theta}) {
-      if (p) {
-        hipFree(p);
-        h->allocs.erase(std::find(h->allocs.begin(), h->allocs.end(), p));
-      }
+    if (h->d_theta) {
+      (void)hipFree(h->d_theta);
+      h->allocs.erase(std::find(h->allocs.begin(), h->allocs.end(), (void*)h->d_theta));
+      h->d_theta = nullptr;
     }
     h->io_cap = 0;
     int rc = dalloc(h, &h->d_theta, need);
@@ -1456,17 +1476,36 @@ int ewh_lnl_batch(ewh_handle* h, const double* theta_host, int32_t B, double* ou
     h->io_cap = need;
   }
   h->d_out = h->d_theta + (size_t)B * std::max(1, h->n_param);
-  if (h->n_param > 0)
-    EWH_HIP(hipMemcpyAsync(h->d_theta, theta_host, sizeof(double) * (size_t)B * h->n_param, hipMemcpyHostToDevice,
-                           h->stream));
-  int rc = ewh_lnl_units_device(h, h->d_theta, B, 0, (long long)h->P * B, h->d_out, h->stream);
-  if (rc) return rc;
-  EWH_HIP(hipMemcpyAsync(out_host, h->d_out, sizeof(double) * B, hipMemcpyDeviceToHost, h->stream));
-  EWH_HIP(hipStreamSynchronize(h->stream));
   return 0;
 }
 
-int ewh_optstat(ewh_handle* h, const double* theta_host, int32_t B, const double* phihat_host, double* rho_host,
+// Cost-balanced contiguous unit ranges (the same rule as
+// enterprise_warp_amd.sharding.unit_ranges).
+std::vector<std::pair<long long, long long>> unit_ranges(const std::vector<double>& cost, int B, int world) {
+  const int P = (int)cost.size();
+  std::vector<std::pair<long long, long long>> out;
+  if (world <= 1) {
+    out.push_back({0, (long long)P * B});
+    return out;
+  }
+  std::vector<double> cum(P + 1, 0.0);
+  for (int p = 0; p < P; ++p) cum[p + 1] = cum[p] + cost[p] * B;
+  std::vector<long long> bounds{0};
+  for (int r = 1; r < world; ++r) {
+    const double target = cum[P] * r / world;
+    int p = (int)(std::upper_bound(cum.begin(), cum.end(), target) - cum.begin()) - 1;
+    p = std::min(std::max(p, 0), P - 1);
+    const double within = cost[p] > 0 ? (target - cum[p]) / cost[p] : 0.0;
+    long long u = (long long)p * B + (long long)std::llround(within);
+    u = std::min<long long>(std::max<long long>(u, bounds.back()), (long long)P * B);
+    bounds.push_back(u);
+  }
+  bounds.push_back((long long)P * B);
+  for (int i = 0; i < world; ++i) out.push_back({bounds[i], bounds[i + 1]});
+  return out;
+}
+
+int ctx_optstat(DevCtx* h, const double* theta_host, int32_t B, const double* phihat_host, double* rho_host,
                 double* sig_host, double* os_host, double* os_sig_host) {
   if (!h || !theta_host || !phihat_host || !os_host || !os_sig_host || B <= 0)
     return set_err(EWH_E_INVALID, "bad arguments");
@@ -1548,22 +1587,273 @@ int ewh_optstat(ewh_handle* h, const double* theta_host, int32_t B, const double
   return 0;
 }
 
-int ewh_last_unit_terms(ewh_handle* h, double* out_host, int32_t B) {
-  if (!h || !out_host || B != h->last_B || !h->d_units) return set_err(EWH_E_INVALID, "no matching previous call");
-  EWH_HIP(hipSetDevice(h->device));
-  EWH_HIP(hipStreamSynchronize(h->stream));
-  EWH_HIP(hipDeviceSynchronize());
-  EWH_HIP(hipMemcpy(out_host, h->d_units, sizeof(double) * (size_t)h->P * B, hipMemcpyDeviceToHost));
+double ctx_unit_cost(const DevCtx* h, int p) {
+  const PsrHost& ps = h->psr[p];
+  if (h->white_fixed) return (double)ps.fx_ld * ps.fx_ld * ps.fx_ld / 3.0;
+  return (double)ps.n_toa * ps.ld * ps.ld + (double)ps.ld * ps.ld * ps.ld / 3.0;
+}
+
+}  // namespace
+
+// The handle: one DevCtx per device of the node (a full replica of the PTA in
+// each device's HBM -- C3 is 0.5 GB of bases against 288 GB), plus pinned
+// host staging shared by all of them.
+struct ewh_handle {
+  std::vector<DevCtx*> ctx;
+  int P = 0, n_param = 0;
+  bool corr = false;
+  // pinned (portable) host staging: theta rows, and the outputs / unit terms
+  double* h_theta = nullptr;
+  size_t h_theta_cap = 0;
+  double* h_out = nullptr;
+  size_t h_out_cap = 0;
+  // last ewh_lnl_batch split: per context, unit range (uncorrelated) or
+  // sample range (correlated)
+  std::vector<std::pair<long long, long long>> last_split;
+  int last_B = 0;
+};
+
+namespace {
+
+int ensure_pinned(double** p, size_t* cap, size_t need) {
+  if (need <= *cap) return 0;
+  if (*p) (void)hipHostFree(*p);
+  *p = nullptr;
+  *cap = 0;
+  hipError_t e = hipHostMalloc((void**)p, std::max<size_t>(need, 1) * sizeof(double), hipHostMallocPortable);
+  if (e != hipSuccess) return set_err(EWH_E_NOMEM, std::string("hipHostMalloc: ") + hipGetErrorString(e));
+  *cap = need;
   return 0;
 }
 
-void ewh_destroy(ewh_handle* h) {
-  if (!h) return;
-  hipSetDevice(h->device);
-  if (h->stream) hipStreamSynchronize(h->stream);
-  for (void* p : h->allocs) hipFree(p);
-  if (h->stream) hipStreamDestroy(h->stream);
-  delete h;
+}  // namespace
+
+extern "C" {
+
+int ewh_version(void) { return EWH_ABI_VERSION; }
+
+const char* ewh_last_error(void) { return g_err.c_str(); }
+
+int ewh_create(const ewh_pta_desc* d, const int32_t* device_ids, int32_t ndev, ewh_handle** out) {
+  if (!out) return set_err(EWH_E_INVALID, "out is NULL");
+  *out = nullptr;
+  if (ndev < 0 || (ndev > 0 && !device_ids) || ndev > 64) return set_err(EWH_E_INVALID, "bad device list");
+  int rc = validate(d);
+  if (rc) return rc;
+  int count = 0;
+  EWH_HIP(hipGetDeviceCount(&count));
+  std::vector<int> ids = ndev ? std::vector<int>(device_ids, device_ids + ndev) : std::vector<int>{0};
+  for (int id : ids)
+    if (id < 0 || id >= count) return set_err(EWH_E_INVALID, "device id " + std::to_string(id) + " out of range");
+  ewh_handle* H = new ewh_handle();
+  H->P = d->n_pulsar;
+  H->n_param = d->n_param;
+  for (int id : ids) {
+    DevCtx* c = nullptr;
+    if ((rc = create_ctx(d, id, &c))) {
+      ewh_destroy(H);
+      return rc;
+    }
+    H->ctx.push_back(c);
+  }
+  H->corr = H->ctx[0]->corr;
+  *out = H;
+  return 0;
 }
+
+int ewh_num_devices(const ewh_handle* H) { return H ? (int)H->ctx.size() : 0; }
+
+int ewh_set_fixed_white(ewh_handle* H, const double* values) {
+  if (!H || !values) return set_err(EWH_E_INVALID, "bad arguments");
+  for (DevCtx* h : H->ctx) {
+    EWH_HIP(hipSetDevice(h->device));
+    size_t off = 0;
+    for (auto& ps : h->psr) {
+      for (int i = 0; i < ps.n_slot; ++i)
+        if (ps.slots[i].idx < 0) ps.slots[i].cval = values[off + i];
+      off += ps.n_slot;
+      if (ps.n_slot)
+        EWH_HIP(hipMemcpyAsync(ps.d_slots, ps.slots.data(), sizeof(ewh_pref) * ps.n_slot, hipMemcpyHostToDevice,
+                               h->stream));
+    }
+    EWH_HIP(hipStreamSynchronize(h->stream));
+    if (h->white_fixed) {
+      int rc = setup_fixed(h);
+      if (rc) return rc;
+    }
+  }
+  return 0;
+}
+
+int ewh_set_kernel_mode(ewh_handle* H, int32_t mode) {
+  if (!H || mode < 0 || mode > 13) return set_err(EWH_E_INVALID, "bad handle / mode");
+  if (mode >= 3 && mode != 7 && !ab_variants_built())
+    return set_err(EWH_E_UNSUPPORTED, "kernel A/B variants are built only into the dev library (make dev)");
+  for (DevCtx* h : H->ctx) h->kernel_mode = mode;
+  return 0;
+}
+
+double ewh_unit_cost(const ewh_handle* H, int32_t p) {
+  if (!H || p < 0 || p >= H->P) return 0.0;
+  return ctx_unit_cost(H->ctx[0], p);
+}
+
+int ewh_lnl_units_device(ewh_handle* H, const double* theta_dev, int32_t B, int64_t u_begin, int64_t u_end,
+                         double* out_dev, void* stream) {
+  if (!H || !theta_dev || !out_dev || B <= 0) return set_err(EWH_E_INVALID, "bad arguments");
+  DevCtx* h = H->ctx[0];
+  if (h->osmode) return set_err(EWH_E_UNSUPPORTED, "an optimal-statistic handle evaluates ewh_optstat only");
+  int rc = ctx_units(h, theta_dev, B, u_begin, u_end, out_dev, (hipStream_t)stream, true);
+  if (rc) return rc;
+  H->last_split.assign(1, {std::max<int64_t>(0, u_begin), std::min<int64_t>((long long)H->P * B, u_end)});
+  H->last_B = B;
+  return 0;
+}
+
+int ewh_lnl_batch(ewh_handle* H, const double* theta_host, int32_t B, double* out_host) {
+  if (!H || !theta_host || !out_host || B <= 0) return set_err(EWH_E_INVALID, "bad arguments");
+  if (H->ctx[0]->osmode) return set_err(EWH_E_UNSUPPORTED, "an optimal-statistic handle evaluates ewh_optstat only");
+  const int nd = (int)H->ctx.size(), np = H->n_param;
+  const long long U = (long long)H->P * B;
+  int rc;
+  if ((rc = ensure_pinned(&H->h_theta, &H->h_theta_cap, (size_t)B * std::max(1, np)))) return rc;
+  if (np > 0) std::memcpy(H->h_theta, theta_host, sizeof(double) * (size_t)B * np);
+  std::vector<std::pair<long long, long long>> split;
+  if (nd == 1 || H->corr) {
+    // samples: contiguous slices (correlated: the cross-pulsar factorisation
+    // needs every pulsar of a sample on one device)
+    for (int i = 0; i < nd; ++i) split.push_back({(long long)B * i / nd, (long long)B * (i + 1) / nd});
+    if ((rc = ensure_pinned(&H->h_out, &H->h_out_cap, (size_t)B))) return rc;
+  } else {
+    std::vector<double> cost(H->P);
+    for (int p = 0; p < H->P; ++p) cost[p] = ctx_unit_cost(H->ctx[0], p);
+    split = unit_ranges(cost, B, nd);
+    if ((rc = ensure_pinned(&H->h_out, &H->h_out_cap, (size_t)U))) return rc;
+  }
+  const bool by_units = !(nd == 1 || H->corr);
+  for (int i = 0; i < nd; ++i) {
+    DevCtx* h = H->ctx[i];
+    const long long a = split[i].first, b = split[i].second;
+    if (b <= a) continue;
+    EWH_HIP(hipSetDevice(h->device));
+    if (by_units) {
+      if ((rc = ensure_io(h, B))) return rc;
+      if (np > 0)
+        EWH_HIP(hipMemcpyAsync(h->d_theta, H->h_theta, sizeof(double) * (size_t)B * np, hipMemcpyHostToDevice,
+                               h->stream));
+      if ((rc = ctx_units(h, h->d_theta, B, a, b, h->d_out, h->stream, false))) return rc;
+      EWH_HIP(hipMemcpyAsync(H->h_out + a, h->d_units + a, sizeof(double) * (size_t)(b - a), hipMemcpyDeviceToHost,
+                             h->stream));
+    } else {
+      const int Bd = (int)(b - a);
+      if ((rc = ensure_io(h, Bd))) return rc;
+      if (np > 0)
+        EWH_HIP(hipMemcpyAsync(h->d_theta, H->h_theta + (size_t)a * np, sizeof(double) * (size_t)Bd * np,
+                               hipMemcpyHostToDevice, h->stream));
+      if ((rc = ctx_units(h, h->d_theta, Bd, 0, (long long)H->P * Bd, h->d_out, h->stream, true))) return rc;
+      EWH_HIP(hipMemcpyAsync(H->h_out + a, h->d_out, sizeof(double) * Bd, hipMemcpyDeviceToHost, h->stream));
+    }
+  }
+  for (int i = 0; i < nd; ++i) {
+    if (split[i].second <= split[i].first) continue;
+    EWH_HIP(hipSetDevice(H->ctx[i]->device));
+    EWH_HIP(hipStreamSynchronize(H->ctx[i]->stream));
+  }
+  if (by_units) {
+    // sum over pulsars in pulsar order: the same left fold as reduce_units_kernel,
+    // so any split gives the single-device result bit for bit
+    for (int b = 0; b < B; ++b) {
+      double s = 0.0;
+      for (int p = 0; p < H->P; ++p) s += H->h_out[(size_t)p * B + b];
+      out_host[b] = s;
+    }
+  } else {
+    std::memcpy(out_host, H->h_out, sizeof(double) * B);
+  }
+  H->last_split = split;
+  H->last_B = B;
+  return 0;
+}
+
+int ewh_optstat(ewh_handle* H, const double* theta_host, int32_t B, const double* phihat_host, double* rho_host,
+                double* sig_host, double* os_host, double* os_sig_host) {
+  if (!H) return set_err(EWH_E_INVALID, "bad arguments");
+  return ctx_optstat(H->ctx[0], theta_host, B, phihat_host, rho_host, sig_host, os_host, os_sig_host);
+}
+
+int ewh_last_unit_terms(ewh_handle* H, double* out_host, int32_t B) {
+  if (!H || !out_host || B != H->last_B || H->last_split.empty()) return set_err(EWH_E_INVALID, "no matching previous call");
+  const int P = H->P, nd = (int)H->last_split.size();
+  const bool by_samples = nd == 1 ? false : H->corr;
+  std::memset(out_host, 0, sizeof(double) * (size_t)P * B);
+  std::vector<double> tmp;
+  for (int i = 0; i < nd; ++i) {
+    DevCtx* h = H->ctx[i];
+    const long long a = H->last_split[i].first, b = H->last_split[i].second;
+    if (b <= a || !h->d_units) continue;
+    EWH_HIP(hipSetDevice(h->device));
+    EWH_HIP(hipStreamSynchronize(h->stream));
+    EWH_HIP(hipDeviceSynchronize());
+    if (nd == 1 && !H->corr) {
+      EWH_HIP(hipMemcpy(out_host, h->d_units, sizeof(double) * (size_t)P * B, hipMemcpyDeviceToHost));
+    } else if (by_samples || nd == 1) {
+      const int Bd = nd == 1 ? B : (int)(b - a);
+      const long long s0 = nd == 1 ? 0 : a;
+      tmp.resize((size_t)P * Bd);
+      EWH_HIP(hipMemcpy(tmp.data(), h->d_units, sizeof(double) * (size_t)P * Bd, hipMemcpyDeviceToHost));
+      for (int p = 0; p < P; ++p)
+        for (int k = 0; k < Bd; ++k) out_host[(size_t)p * B + s0 + k] = tmp[(size_t)p * Bd + k];
+    } else {
+      EWH_HIP(hipMemcpy(out_host + a, h->d_units + a, sizeof(double) * (size_t)(b - a), hipMemcpyDeviceToHost));
+    }
+  }
+  return 0;
+}
+
+void ewh_destroy(ewh_handle* H) {
+  if (!H) return;
+  for (DevCtx* c : H->ctx) destroy_ctx(c);
+  if (H->h_theta) (void)hipHostFree(H->h_theta);
+  if (H->h_out) (void)hipHostFree(H->h_out);
+  delete H;
+}
+
+#ifdef EWH_DEV
+// ---- dev library only (make dev): intermediate quantities for diagnostics ----
+// G = T_aug^T N^-1 T_aug of pulsar p for samples [0, B) (B <= the varying-WN
+// chunk), row-major ld x ld per sample; returns ld (or a negative code).
+int ewh_dev_gram(ewh_handle* H, int32_t p, const double* theta_host, int32_t B, double* G_out) {
+  DevCtx* h = H->ctx[0];
+  if (p < 0 || p >= h->P || B <= 0) return set_err(EWH_E_INVALID, "bad arguments");
+  int rc;
+  EWH_HIP(hipSetDevice(h->device));
+  const bool wf = h->white_fixed;
+  h->white_fixed = false;
+  rc = ensure_var_scratch(h, B);
+  h->white_fixed = wf;
+  if (rc) return rc;
+  if (B > h->chunk) return set_err(EWH_E_INVALID, "B exceeds the varying-WN chunk");
+  if ((rc = ensure_io(h, B))) return rc;
+  if (h->n_param > 0)
+    EWH_HIP(hipMemcpy(h->d_theta, theta_host, sizeof(double) * (size_t)B * h->n_param, hipMemcpyHostToDevice));
+  if ((rc = run_white(h, p, h->d_theta, h->n_param, 0, B))) return rc;
+  EWH_HIP(hipStreamSynchronize(h->stream));
+  const int ld = h->psr[p].ld;
+  EWH_HIP(hipMemcpy(G_out, h->d_G, sizeof(double) * (size_t)B * ld * ld, hipMemcpyDeviceToHost));
+  return ld;
+}
+
+// the cached reduced matrix S_p (fx_ld x fx_ld) and K_p of a fixed-WN handle; returns fx_ld
+int ewh_dev_reduced(ewh_handle* H, int32_t p, double* S_out, double* K_out) {
+  DevCtx* h = H->ctx[0];
+  if (!h->white_fixed || p < 0 || p >= h->P) return set_err(EWH_E_INVALID, "bad arguments");
+  EWH_HIP(hipSetDevice(h->device));
+  EWH_HIP(hipDeviceSynchronize());
+  const int n = h->psr[p].fx_ld;
+  EWH_HIP(hipMemcpy(S_out, h->psr[p].d_S, sizeof(double) * (size_t)n * n, hipMemcpyDeviceToHost));
+  EWH_HIP(hipMemcpy(K_out, h->d_fxK + p, sizeof(double), hipMemcpyDeviceToHost));
+  return n;
+}
+#endif
 
 }  // extern "C"

@@ -31,7 +31,7 @@ class PTA:
         if len(set(names)) != len(names):
             raise ValueError("duplicate pulsar names in PTA")
         self._engine = None
-        self._engine_device = None
+        self._engine_devices = None
         self._rebuild_params()
 
     # ------------------------------------------------------------------ params
@@ -91,18 +91,26 @@ class PTA:
         noise files name EQUAD `{psr}_{backend}_log10_equad` while
         TNEquadNoise's parameter is `..._log10_tnequad`; a `_log10_equad` key
         fills the matching `_log10_tnequad` Constant when that key is absent."""
-        changed = False
         keyed = dict(params)
         for k, v in params.items():
             if k.endswith("_log10_equad"):
                 keyed.setdefault(k[: -len("_log10_equad")] + "_log10_tnequad", v)
+        changed = set()
         for p in self._all.values():
             if isinstance(p, parameter.ConstantParameter) and p.name in keyed:
                 val = float(keyed[p.name])
                 if p.value != val:
+                    was_set = p.value is not None
                     p.value = val
-                    changed = True
-        if changed:
+                    changed.add(p.name if was_set else None)
+        if not changed:
+            return
+        white = {p.name for c in self._collections for w in c.white for p in w.params}
+        if self._engine is not None and None not in changed and changed <= white:
+            # new white-noise constants only: recompute the cached TNT etc. in
+            # place (ewh_set_fixed_white) instead of rebuilding the engine
+            self._engine.set_fixed_white(self)
+        else:
             self._drop_engine()
 
     def get_lnprior(self, params):
@@ -149,15 +157,21 @@ class PTA:
         th = self._theta(X)
         return self.engine().lnl_batch(th)
 
-    def engine(self, device=None):
+    def engine(self, device=None, devices=None):
         """The device-resident likelihood (created on first use, after
-        set_default_params; re-created when constants change)."""
-        if device is None:
-            device = self._engine_device if self._engine_device is not None else 0
-        if self._engine is None or self._engine_device != device:
+        set_default_params; re-created when the device list or non-white
+        constants change).  devices: HIP device ids the handle spreads every
+        batch over (get_lnlikelihood_batch then uses the whole node);
+        device: shorthand for [device].  Default: the current list, else [0]."""
+        if devices is None and device is not None:
+            devices = [device]
+        if devices is None:
+            devices = self._engine_devices if self._engine_devices is not None else [0]
+        devices = [int(d) for d in devices]
+        if self._engine is None or self._engine_devices != devices:
             self._drop_engine()
-            self._engine = Engine(self, device)
-            self._engine_device = device
+            self._engine = Engine(self, devices)
+            self._engine_devices = devices
         return self._engine
 
     def _drop_engine(self):
@@ -234,29 +248,7 @@ class PTA:
         corr = self.correlated()
         for c in self._collections:
             psr = c.psr
-            n = len(psr.toas)
-            slots, slot_of = [], {}
-
-            def slot(p):
-                if p.name not in slot_of:
-                    slot_of[p.name] = len(slots)
-                    slots.append(self._pref(p))
-                return slot_of[p.name]
-
-            efac = np.full(n, -1, np.int32)
-            equad = np.full(n, -1, np.int32)
-            for w in c.white:
-                if w.kind == "ecorr":
-                    continue
-                tgt = efac if w.kind == "efac" else equad
-                for key, mask in w.masks.items():
-                    tgt[mask] = slot(w.pars[key])
-            if np.any(efac < 0):
-                raise ValueError(f"{c.name}: some TOAs are not covered by the efac selection")
-            eps = c.ecorr_epochs()
-            ep_start = np.array([e[0] for e in eps], np.int32)
-            ep_stop = np.array([e[1] for e in eps], np.int32)
-            ep_slot = np.array([slot(e[2]) for e in eps], np.int32)
+            slots, efac, equad, ep_start, ep_stop, ep_slot = self._white_tables(c)
             # column order: [leading constant-phi | own | common (g order)] when the
             # PTA has a correlated common process (the device keeps the common
             # block for the cross-pulsar factorisation, include/ewarp_hip.h)
@@ -288,6 +280,35 @@ class PTA:
                             ep_start=ep_start, ep_stop=ep_stop, ep_slot=ep_slot, spec=spec))
         return out
 
+    def _white_tables(self, c):
+        """White-noise slot table of one pulsar (theta column or constant per
+        distinct efac / equad / ecorr parameter) and the per-TOA / per-epoch
+        slot indices (include/ewarp_hip.h ewh_pulsar_desc)."""
+        n = len(c.psr.toas)
+        slots, slot_of = [], {}
+
+        def slot(p):
+            if p.name not in slot_of:
+                slot_of[p.name] = len(slots)
+                slots.append(self._pref(p))
+            return slot_of[p.name]
+
+        efac = np.full(n, -1, np.int32)
+        equad = np.full(n, -1, np.int32)
+        for w in c.white:
+            if w.kind == "ecorr":
+                continue
+            tgt = efac if w.kind == "efac" else equad
+            for key, mask in w.masks.items():
+                tgt[mask] = slot(w.pars[key])
+        if np.any(efac < 0):
+            raise ValueError(f"{c.name}: some TOAs are not covered by the efac selection")
+        eps = c.ecorr_epochs()
+        ep_start = np.array([e[0] for e in eps], np.int32)
+        ep_stop = np.array([e[1] for e in eps], np.int32)
+        ep_slot = np.array([slot(e[2]) for e in eps], np.int32)
+        return slots, efac, equad, ep_start, ep_stop, ep_slot
+
     # ---------------------------------------------------------------- helpers
     def constant_values(self):
         return {p.name: p.value for p in self._all.values() if isinstance(p, parameter.ConstantParameter)}
@@ -311,14 +332,17 @@ def _as_ptr(a, ctype):
 
 
 class Engine:
-    """Owner of one libewarp_hip handle (one device)."""
+    """Owner of one libewarp_hip handle (one or several devices)."""
 
-    def __init__(self, pta, device=0, optstat=None):
-        """optstat: None, or {"signal": name, "orf": P x P matrix} for an
-        optimal-statistic handle (ewh_optstat; see enterprise_warp_amd.optstat)."""
+    def __init__(self, pta, devices=0, optstat=None):
+        """devices: a HIP device id or a list of them (one replica per entry;
+        a repeated id gives two contexts on one device).  optstat: None, or
+        {"signal": name, "orf": P x P matrix} for an optimal-statistic handle
+        (ewh_optstat; see enterprise_warp_amd.optstat)."""
         self.lib = _lib.load()
         self.pta = pta
-        self.device = device
+        self.devices = [int(devices)] if np.isscalar(devices) else [int(d) for d in devices]
+        self.device = self.devices[0]
         lay = pta.layout(common_last=optstat["signal"] if optstat else None)
         self.n_pulsar = len(lay)
         self.n_param = pta._nparam
@@ -367,8 +391,10 @@ class Engine:
         d = _lib.PtaDesc(_lib.EWH_ABI_VERSION, len(lay), self.n_param, int(self.white_fixed), descs,
                          C.pointer(common) if common is not None else None)
         h = C.c_void_p()
-        _lib.check(self.lib.ewh_create(C.byref(d), int(device), C.byref(h)))
+        ids = (C.c_int32 * len(self.devices))(*self.devices)
+        _lib.check(self.lib.ewh_create(C.byref(d), ids, len(self.devices), C.byref(h)))
         self.h = h
+        self.n_slots = [len(L["slots"]) for L in lay]
         del keep
 
     def lnl_batch(self, theta):
@@ -377,6 +403,37 @@ class Engine:
         out = np.empty(B)
         _lib.check(self.lib.ewh_lnl_batch(self.h, _as_ptr(theta, C.c_double), B, _as_ptr(out, C.c_double)))
         return out
+
+    def set_fixed_white(self, pta):
+        """Push the PTA's current white-noise constants (ewh_set_fixed_white)."""
+        vals = []
+        for c in pta.signal_collections:
+            vals.extend(cv for _, cv in pta._white_tables(c)[0])
+        arr = np.ascontiguousarray(vals if vals else [0.0], dtype=float)
+        _lib.check(self.lib.ewh_set_fixed_white(self.h, _as_ptr(arr, C.c_double)))
+
+    def num_devices(self):
+        return int(self.lib.ewh_num_devices(self.h))
+
+    def dev_gram(self, p, theta):
+        """Dev library only: G = T_aug^T N^-1 T_aug of pulsar p per sample."""
+        theta = np.ascontiguousarray(np.atleast_2d(theta), dtype=float)
+        B = theta.shape[0]
+        ld = 16 * ((self.pta.signal_collections[p].T.shape[1] + 1 + 15) // 16)
+        G = np.empty((B, ld, ld))
+        rc = self.lib.ewh_dev_gram(self.h, int(p), _as_ptr(theta, C.c_double), B, _as_ptr(G, C.c_double))
+        if rc < 0:
+            _lib.check(rc)
+        return G
+
+    def dev_reduced(self, p, n):
+        """Dev library only: the cached reduced matrix S_p (n x n) and K_p."""
+        S = np.empty((n, n))
+        K = np.empty(1)
+        rc = self.lib.ewh_dev_reduced(self.h, int(p), _as_ptr(S, C.c_double), _as_ptr(K, C.c_double))
+        if rc < 0:
+            _lib.check(rc)
+        return S, float(K[0])
 
     def lnl_units_device(self, theta_ptr, B, u0, u1, out_ptr, stream=None):
         _lib.check(self.lib.ewh_lnl_units_device(self.h, C.c_void_p(theta_ptr), int(B), int(u0), int(u1),

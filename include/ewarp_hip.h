@@ -13,13 +13,18 @@
  *   ewh_create          replaces signal_base.PTA.__init__ + the white-noise
  *                       cache of LogLikelihood (enterprise_warp.py:502-508):
  *                       uploads every pulsar's basis, residuals, TOA errors,
- *                       white-noise tables and spectral table; when white
- *                       noise is fixed (Constant efac/equad/ecorr set from
- *                       noise files, enterprise_warp.py:504-508) it also
- *                       computes and caches T^T N^-1 T, T^T N^-1 r, r^T N^-1 r,
- *                       log|N| and the timing-model elimination on device.
+ *                       white-noise tables and spectral table to each listed
+ *                       device; when white noise is fixed (Constant
+ *                       efac/equad/ecorr set from noise files,
+ *                       enterprise_warp.py:504-508) it also computes and
+ *                       caches T^T N^-1 T, T^T N^-1 r, r^T N^-1 r, log|N| and
+ *                       the timing-model elimination on each device.
+ *   ewh_set_fixed_white replaces pta.set_default_params(noisedict)
+ *                       (enterprise_warp.py:504-508) for new white-noise
+ *                       constants: recomputes the cache in place.
  *   ewh_lnl_batch       replaces B calls of pta.get_lnlikelihood
- *                       (bilby_warp.py:35) — host theta in, host lnL out.
+ *                       (bilby_warp.py:35) — host theta in, host lnL out,
+ *                       spread over every device of the handle.
  *   ewh_lnl_units_device  the same on device buffers for a contiguous range
  *                       of (pulsar, sample) units; used for multi-GPU
  *                       sharding (partial sums, then an RCCL all-reduce).
@@ -49,7 +54,7 @@
 extern "C" {
 #endif
 
-#define EWH_ABI_VERSION 4
+#define EWH_ABI_VERSION 5
 
 enum ewh_status {
   EWH_OK = 0,
@@ -156,13 +161,33 @@ typedef struct ewh_pta_desc {
 
 typedef struct ewh_handle ewh_handle;
 
-/* Build the device-resident PTA on HIP device `device`. */
-int ewh_create(const ewh_pta_desc* desc, int device, ewh_handle** out);
+/* Build the device-resident PTA on the HIP devices device_ids[0..ndev-1]
+ * (NULL / 0: device 0).  Each device holds a full replica (bases, tables,
+ * fixed-WN cache) and its own stream; a device id may repeat (two contexts
+ * on one device: the split is then exercised on a one-GPU host). */
+int ewh_create(const ewh_pta_desc* desc, const int32_t* device_ids, int32_t ndev, ewh_handle** out);
 
-/* lnL for B samples: theta_host [B x n_param], out_host [B]. Synchronous. */
+/* Number of device contexts of the handle. */
+int ewh_num_devices(const ewh_handle* h);
+
+/* New constant white-noise values (the in-place form of the reference's
+ * pta.set_default_params(noisedict), enterprise_warp.py:504-508).
+ * values: for each pulsar in descriptor order, its n_slot entries in slot
+ * order; the value of every constant slot (idx < 0) is replaced, theta-
+ * referencing slots ignore theirs.  A fixed-white-noise handle recomputes
+ * T^T N^-1 T, d, r^T N^-1 r, log|N| and the timing-model elimination on
+ * every device; bases and layout are unchanged. Synchronous. */
+int ewh_set_fixed_white(ewh_handle* h, const double* values);
+
+/* lnL for B samples: theta_host [B x n_param], out_host [B]. Synchronous.
+ * Several devices: uncorrelated / CURN models split the (pulsar, sample)
+ * units into cost-balanced contiguous ranges (one per device) and sum the
+ * per-pulsar terms on the host in pulsar order (bit-identical to one
+ * device); a correlated common process splits the samples.  theta is staged
+ * through pinned host memory owned by the handle. */
 int ewh_lnl_batch(ewh_handle* h, const double* theta_host, int32_t B, double* out_host);
 
-/* Device variant on a contiguous range [unit_begin, unit_end) of units
+/* Device variant (the handle's first device) on a contiguous range [unit_begin, unit_end) of units
  * u = pulsar * B + sample.  With a correlated common process the range must
  * be the whole batch [0, n_pulsar * B) (shard samples across devices by
  * passing each one its own theta rows instead).  out_dev[b] = sum of the unit lnL terms of sample
@@ -173,7 +198,7 @@ int ewh_lnl_units_device(ewh_handle* h, const double* theta_dev, int32_t B,
                          int64_t unit_begin, int64_t unit_end, double* out_dev,
                          void* stream);
 
-/* Optimal statistic (the reference's results.py:653-795 ->
+/* Optimal statistic (first device of the handle; the reference's results.py:653-795 ->
  * enterprise_extensions OptimalStatistic.compute_os) for B noise-parameter
  * draws, on a handle created with common->kind == EWH_COMMON_OPTSTAT (fixed
  * white noise): per pulsar X = F^T P^-1 r, Z = F^T P^-1 F (F = the common
@@ -210,7 +235,9 @@ double ewh_unit_cost(const ewh_handle* h, int32_t pulsar);
  * 7 = default Cholesky with the round-1 kernels elsewhere: the
  * contraction (varying white noise: separate epoch-sum kernel, unpipelined
  * tiles) instead of the pipelined one and, for a correlated common process,
- * the right-looking dense update and the LDS Gauss-Jordan M_g inverse. */
+ * the right-looking dense update and the LDS Gauss-Jordan M_g inverse.
+ * Modes 3-6 and 8-13 exist only in the dev library (`make dev`:
+ * libewarp_hip_dev.so); the product library returns EWH_E_UNSUPPORTED. */
 int ewh_set_kernel_mode(ewh_handle* h, int32_t mode);
 
 void ewh_destroy(ewh_handle* h);

@@ -1,0 +1,426 @@
+"""TEST INFRASTRUCTURE ONLY — the likelihood in the DEVICE's order of operations.
+
+`enterprise_ref` restates enterprise's own order (the full Sigma = TNT +
+diag(1/phi) factored by LAPACK `cho_factor`, timing-model columns included).
+libewarp_hip.so computes the same quantity in another order
+(enterprise_warp_amd/csrc/ewarp_hip.hip):
+
+* the residual is the LAST column of the basis, so one Gram matrix
+  G = [T r]^T N^-1 [T r] carries TNT, d = TNr and rNr, and the last pivot of
+  the factorisation of G + diag(1/phi, 0) is q = rNr - d^T Sigma^-1 d;
+* fixed white noise: the constant-phi (timing-model, phi = 1e40) leading block
+  is eliminated ONCE by a sequential Cholesky (`schur_kernel`), leaving the
+  reduced matrix S with the residual last; per sample only
+  S + diag(1/phi_own, 0) is factored;
+* the factorisation is an LDL^T in 16-wide block rows (`chol_mfma_kernel`:
+  diagonal block eliminated pivot by pivot, the rest of the block row by
+  L^-1, trailing update A -= U^T U with U = D^-1/2 L^-1 A);
+* a correlated common process (HD / monopole / dipole ORF) keeps each
+  pulsar's common block after eliminating its own columns, inverts
+  M_g = Gamma phi_c(g) + diag(phi_own(., g)) per common column by
+  Gauss-Jordan, and factors the dense Sigma_c = blockdiag(S^G_a) + [M_g^-1]
+  in 64-wide block rows;
+* lnL_p = K - q/2 - 1/2 sum log d_k - 1/2 sum log phi.
+
+Every function takes a numpy dtype.  With `np.float64` this is the device's
+ordering in fp64 (used to measure how far two correct fp64 orderings of the
+same likelihood drift apart on each golden sample: the `spread` stored in the
+fixtures).  With `np.longdouble` (x86 80-bit extended, eps 1.1e-19) it is a
+near-exact value of the same likelihood for the same fp64 inputs, against
+which both orderings' errors are measured (tests/golden/make_golden.py).
+
+Model tables (bases, selections, epochs, spectra, parameter names) come from
+`enterprise_ref.OraclePulsar`; only the arithmetic order differs.
+"""
+import numpy as np
+
+from .enterprise_ref import FYR, OraclePTA, orf_value
+
+TM_PHI = 1e40        # [ent] utils.tm_prior
+
+
+def _cast(params, dt):
+    out = {}
+    for k, v in params.items():
+        if v is None:
+            continue
+        a = np.asarray(v)
+        out[k] = a.astype(dt) if a.ndim else dt(a)
+    return out
+
+
+def _spectrum(g, p, dt):
+    """phi of one GP signal on its own columns, in dtype dt (the formulas of
+    enterprise_ref.powerlaw / powerlaw_bpl / free_spectrum)."""
+    f = np.asarray(g["f"], dtype=dt)
+    val = lambda ref: dt(ref[1]) if ref[0] == "const" else p[ref[1]]  # noqa: E731
+    nm = g["names"]
+    comp = g["components"]
+    df = np.diff(np.concatenate((np.zeros(1, dt), f[::comp])))
+    df = np.repeat(df, comp)
+    pi2 = dt(np.pi) ** 2 if dt is np.float64 else np.arccos(dt(-1)) ** 2
+    fyr = dt(FYR)
+    if g["spectrum"] == "powerlaw":
+        A, gam = val(nm["log10_A"]), val(nm["gamma"])
+        return dt(10) ** (2 * A) / 12 / pi2 * fyr ** (gam - 3) * f ** (-gam) * df
+    if g["spectrum"] == "turnover":
+        A, gam, fc = val(nm["log10_A"]), val(nm["gamma"]), val(nm["fc"])
+        if fc < 0:
+            fc = dt(10) ** fc
+        return dt(10) ** (2 * A) / 12 / pi2 * fyr ** (-3) * ((f + fc) / fyr) ** (-gam) * df
+    rho = val(nm["log10_rho"])
+    return np.repeat(dt(10) ** (2 * np.asarray(rho, dtype=dt)), 2)
+
+
+def phi_columns(pp, p, dt, with_common=True):
+    """Per-column phi of one pulsar ([ent] SignalCollection.get_phi), in dt.
+    with_common=False leaves out a correlated common signal (it lives in the
+    cross-pulsar M_g blocks of the device)."""
+    phi = np.zeros(pp.T.shape[1], dtype=dt)
+    for g in pp.gps:
+        if g["kind"] == "tm":
+            phi[g["idx"]] += dt(TM_PHI)
+            continue
+        if g.get("orf"):
+            if with_common:
+                pos = np.asarray(pp.psr.pos, float)
+                phi[g["idx"]] += dt(orf_value(g["orf"], pos, pos)) * _spectrum(g, p, dt)
+            continue
+        phi[g["idx"]] += _spectrum(g, p, dt)
+    return phi
+
+
+def _fma(a, b, c):
+    """fp64 fused multiply-add, emulated through the x87 extended product
+    (double rounding differs from a true FMA on ~1 in 2^11 operations)."""
+    return (np.asarray(a, dtype=np.longdouble) * b + c).astype(np.float64)
+
+
+def gram_device_fma(pp, p):
+    """fp64 Gram in the contraction kernels' accumulation order
+    (contract2_kernel): per entry one accumulator, TOA rows (padded to whole
+    32-row tiles) taken 4 at a time as sequential FMAs of (w_t T_ti) T_tj;
+    ECORR epoch sums s_e as an FMA chain over the epoch's TOAs, then the
+    epoch rows with weights -beta_e through the same accumulator."""
+    n = len(pp.r)
+    Dd = np.zeros(n)
+    sig2 = np.asarray(pp.sigma, float) ** 2
+    for k, masks, names in pp.white:
+        for key, m in masks.items():
+            if k == "efac":
+                ef = float(p[names[key]])
+                Dd[m] += (ef * ef) * sig2[m]
+            elif k == "tnequad":
+                Dd[m] += 10.0 ** (2.0 * float(p[names[key]]))
+    w = 1.0 / Dd
+    T = np.asarray(pp.basis({k: float(v) for k, v in p.items() if np.ndim(v) == 0}), dtype=float)
+    X = np.concatenate([T, np.asarray(pp.r, float)[:, None]], axis=1)
+    m1 = X.shape[1]
+    acc = np.zeros((m1, m1))
+
+    def rows(acc, R, wr):
+        npad = (len(R) + 31) // 32 * 32
+        Rp = np.zeros((npad, m1))
+        Rp[:len(R)] = R
+        wp = np.zeros(npad)
+        wp[:len(R)] = wr
+        A = Rp * wp[:, None]
+        for t in range(npad):
+            acc = _fma(A[t][:, None], Rp[t][None, :], acc)
+        return acc
+
+    acc = rows(acc, X, w)
+    ldn = np.sum(np.log(Dd))
+    if pp.ecorr:
+        S, nb = [], []
+        for slc, nm in pp.ecorr:
+            J = 10.0 ** (2.0 * float(p[nm]))
+            sw = 0.0
+            e = np.zeros(m1)
+            for t in range(slc.start, slc.stop):
+                sw = sw + w[t]
+                e = _fma(np.full(m1, w[t]), X[t], e)
+            beta = 1.0 / (sw + 1.0 / J)
+            S.append(e)
+            nb.append(-beta)
+            ldn += np.log(J) - np.log(beta)
+        acc = rows(acc, np.array(S), np.array(nb))
+    return acc, ldn
+
+
+def gram(pp, p, dt, mode="blas"):
+    """G = [T r]^T N^-1 [T r] (ShermanMorrison form of EcorrKernelNoise) and
+    log|N|, in dt.  mode "blas": one matrix product; "reverse": the TOAs
+    summed in reverse order; "device": gram_device_fma (fp64 only)."""
+    if mode == "device":
+        return gram_device_fma(pp, p)
+    n = len(pp.r)
+    D = np.zeros(n, dtype=dt)
+    sig2 = np.asarray(pp.sigma, dtype=dt) ** 2
+    for k, masks, names in pp.white:
+        for key, m in masks.items():
+            if k == "efac":
+                D[m] += p[names[key]] ** 2 * sig2[m]
+            elif k == "tnequad":
+                D[m] += dt(10) ** (2 * p[names[key]])
+    T = np.asarray(pp.basis({k: float(v) for k, v in p.items() if np.ndim(v) == 0}), dtype=dt)
+    X = np.concatenate([T, np.asarray(pp.r, dtype=dt)[:, None]], axis=1)
+    if mode == "reverse":
+        X, D = X[::-1], D[::-1]
+    W = X / D[:, None]
+    G = X.T @ W
+    if mode == "reverse":
+        X, D = X[::-1], D[::-1]
+    ldn = np.sum(np.log(D))
+    for slc, nm in pp.ecorr:
+        J = dt(10) ** (2 * p[nm])
+        ni = 1 / D[slc]
+        beta = 1 / (np.sum(ni) + 1 / J)
+        s = ni @ X[slc]
+        G -= beta * np.outer(s, s)
+        ldn += np.log(J) - np.log(beta)
+    return G, ldn
+
+
+def lead_schur(G, nlead, phi_lead, device=False):
+    """`schur_kernel`: add 1/phi to the leading block's diagonal, eliminate it
+    by a sequential Cholesky; returns (reduced G, sum log L_kk, ok).
+    device=True (fp64): the kernel's arithmetic -- row k scaled by 1/sqrt(pivot),
+    updates as fused multiply-adds."""
+    G = G.copy()
+    idx = np.arange(nlead)
+    G[idx, idx] += 1 / phi_lead
+    logdet = G.dtype.type(0)
+    ok = True
+    for k in range(nlead):
+        piv = G[k, k]
+        ok &= bool(piv > 0)
+        d = np.sqrt(piv)
+        logdet += np.log(d)
+        if device:
+            row = G[k, k + 1:] * (1.0 / d)
+            G[k + 1:, k + 1:] = _fma(-row[:, None], row[None, :], G[k + 1:, k + 1:])
+        else:
+            row = G[k, k + 1:] / d
+            G[k + 1:, k + 1:] -= np.outer(row, row)
+    return G[nlead:, nlead:], logdet, ok
+
+
+def ldl_blocked(A, npiv, bs=16):
+    """LDL^T in bs-wide block rows (the register kernels' blocked panel):
+    within a block row the pivots are eliminated one at a time across the
+    whole row (= L^-1 applied to the off-diagonal blocks), the row is scaled
+    to U = D^-1/2 V and the trailing matrix takes A -= U^T U.  Pivots are
+    0..npiv-1; the rest of the matrix (the residual corner / a kept block) is
+    returned updated.  Returns (pivots d, updated A)."""
+    A = A.copy()
+    n = A.shape[0]
+    d = []
+    for k0 in range(0, npiv, bs):
+        k1 = min(k0 + bs, n)
+        kend = min(k1, npiv)
+        for k in range(k0, kend):
+            dk = A[k, k]
+            d.append(dk)
+            w = A[k, k + 1:] / dk
+            # rows k+1..k1-1 of this block row take row k (columns > k)
+            A[k + 1:k1, k + 1:] -= np.outer(A[k + 1:k1, k], w)
+        if k1 < n:
+            dv = np.array(d[k0:kend], dtype=A.dtype)
+            U = A[k0:kend, k1:] / np.sqrt(dv)[:, None]
+            A[k1:, k1:] -= U.T @ U
+    return np.array(d, dtype=A.dtype), A
+
+
+def chol_unblocked(A, npiv):
+    """Sequential right-looking Cholesky (scipy cho_factor's pivot order, no
+    blocking): pivots d_k = L_kk^2 and the updated trailing corner."""
+    A = A.copy()
+    d = []
+    for k in range(npiv):
+        dk = A[k, k]
+        d.append(dk)
+        row = A[k, k + 1:] / np.sqrt(dk)
+        A[k + 1:, k + 1:] -= np.outer(row, row)
+    return np.array(d, dtype=A.dtype), A
+
+
+def _block_layout(nown, ncom):
+    """Reduced layout of the device (ewarp_hip.hip ewh_create):
+    [own | pad | r] or, with a common block, [own | pad to 16 | common | pad | r].
+    Returns (size, gstart)."""
+    if ncom:
+        gstart = 16 * ((nown + 15) // 16)
+        return 16 * ((gstart + ncom + 1 + 15) // 16), gstart
+    return 16 * ((nown + 1 + 15) // 16), nown
+
+
+class DeviceOrderPTA:
+    """The device's ordering of the same likelihood (fixed or varying white
+    noise, uncorrelated / CURN or correlated common process)."""
+
+    def __init__(self, psrs, terms_per_psr, fixed_params=None, dtype=np.float64, gram_mode="blas",
+                 factor="ldl16"):
+        """gram_mode: "blas" | "reverse" | "device" (the contraction kernels'
+        FMA order, fp64); factor: "ldl16" (the register kernels' blocked
+        LDL^T) | "chol" (unblocked Cholesky).  The default is the device
+        order; the variants are further correct fp64 orderings used to
+        measure the spread of a sample (tests/golden/make_golden.py)."""
+        self.o = OraclePTA(psrs, terms_per_psr, fixed_params=None)
+        self.dt = dtype
+        self.gram_mode = gram_mode
+        self.factor = ldl_blocked if factor == "ldl16" else (lambda A, npiv, bs=16: chol_unblocked(A, npiv))
+        self.pulsars = self.o.pulsars
+        self.nlead = []
+        for pp in self.pulsars:
+            tm = [g for g in pp.gps if g["kind"] == "tm"]
+            nl = len(set(tm[0]["idx"])) if tm else 0
+            if tm and sorted(set(tm[0]["idx"])) != list(range(nl)):
+                raise ValueError("timing-model columns must lead the basis")
+            self.nlead.append(nl)
+        self.white_fixed = fixed_params is not None and not any(pp.basis_params for pp in self.pulsars)
+        self.cache = None
+        if self.white_fixed:
+            p = _cast(fixed_params, dtype)
+            self.cache = [self._reduce(i, p) for i in range(len(self.pulsars))]
+
+    def correlated(self):
+        return self.o.correlated()
+
+    # ---- per pulsar: G, lead elimination, reduced layout -----------------
+    def _common_cols(self, pp):
+        for g in pp.gps:
+            if g.get("orf"):
+                return list(g["idx"])
+        return []
+
+    def _reduce(self, i, p):
+        """Gram + timing-model elimination of pulsar i: (S in the device's
+        reduced layout, K, ok, own column ids, common column ids)."""
+        pp = self.pulsars[i]
+        dt = self.dt
+        G, ldn = gram(pp, p, dt, self.gram_mode)
+        m = pp.T.shape[1]
+        nl = self.nlead[i]
+        phi_lead = np.full(nl, TM_PHI, dtype=dt)           # constant-phi leading block
+        com = self._common_cols(pp) if self.correlated() else []
+        own = [j for j in range(nl, m) if j not in set(com)]
+        Sr, logdet, ok = lead_schur(G, nl, phi_lead, device=self.gram_mode == "device")
+        K = -ldn / 2 - logdet - np.sum(np.log(phi_lead)) / 2
+        # Sr indexes columns nl..m (r last); lay it out as the device does
+        size, gstart = _block_layout(len(own), len(com))
+        pos = np.full(size, -1)
+        pos[:len(own)] = [j - nl for j in own]
+        pos[gstart:gstart + len(com)] = [j - nl for j in com]
+        pos[size - 1] = m - nl
+        S = np.zeros((size, size), dtype=dt)
+        S[np.arange(size), np.arange(size)] = 1
+        live = pos >= 0
+        S[np.ix_(live, live)] = Sr[np.ix_(pos[live], pos[live])]
+        return S, K, ok, own, com, gstart
+
+    # ---- lnL ------------------------------------------------------------
+    def lnlikelihood(self, params):
+        p = _cast(params, self.dt)
+        if self.correlated():
+            return float(self._lnl_correlated(p))
+        tot = self.dt(0)
+        for i, pp in enumerate(self.pulsars):
+            S, K, ok, own, _, _ = self.cache[i] if self.white_fixed else self._reduce(i, p)
+            phi = phi_columns(pp, p, self.dt)[own]
+            A = S.copy()
+            idx = np.arange(len(own))
+            A[idx, idx] += 1 / phi
+            d, A = self.factor(A, A.shape[0] - 1)
+            if not ok or not np.all(d > 0):
+                return -np.inf
+            q = A[-1, -1]
+            tot += K - q / 2 - np.sum(np.log(d)) / 2 - np.sum(np.log(phi)) / 2
+        return float(tot)
+
+    def min_eig(self, params):
+        """Conditioning of what the device factors for this sample: min over
+        pulsars of lambda_min of the unit-diagonal-scaled S + diag(1/phi_own)
+        (own columns, timing model eliminated), fp64.  Informational: near 0
+        means two correct fp64 orderings may differ widely (the `spread`)."""
+        if self.correlated():
+            return float("nan")
+        p = _cast(params, np.float64)
+        mins = []
+        for i, pp in enumerate(self.pulsars):
+            S, K, ok, own, _, _ = self.cache[i] if self.white_fixed else self._reduce(i, p)
+            S = np.array(S[:len(own), :len(own)], dtype=np.float64)
+            S[np.arange(len(own)), np.arange(len(own))] += 1 / np.asarray(phi_columns(pp, p, np.float64)[own])
+            sc = 1 / np.sqrt(np.abs(np.diag(S)))
+            mins.append(np.linalg.eigvalsh(S * sc[:, None] * sc[None, :])[0])
+        return float(min(mins))
+
+    def _lnl_correlated(self, p):
+        dt = self.dt
+        P = len(self.pulsars)
+        keeps, local = [], dt(0)
+        nc = None
+        own_phi_common = []
+        for i, pp in enumerate(self.pulsars):
+            S, K, ok, own, com, gstart = self.cache[i] if self.white_fixed else self._reduce(i, p)
+            nc = len(com)
+            phi_all = phi_columns(pp, p, dt, with_common=False)
+            phi = phi_all[own]
+            own_phi_common.append(phi_all[com])
+            A = S.copy()
+            idx = np.arange(len(own))
+            A[idx, idx] += 1 / phi
+            d, A = ldl_blocked(A, gstart)
+            if not ok or not np.all(d > 0):
+                return -np.inf
+            local += K - np.sum(np.log(d)) / 2 - np.sum(np.log(phi)) / 2
+            kb = A[gstart:, gstart:]
+            keeps.append((kb[:nc, :nc], kb[:nc, -1], kb[-1, -1]))
+        # common spectrum and ORF
+        pp0 = self.pulsars[0]
+        gc = next(g for g in pp0.gps if g.get("orf"))
+        phic = _spectrum(gc, p, dt)
+        pos = [np.asarray(pp.psr.pos, float) for pp in self.pulsars]
+        Gam = np.array([[orf_value(gc["orf"], pos[a], pos[b]) for b in range(P)] for a in range(P)], dtype=dt)
+        N = P * nc
+        Sc = np.zeros((N + 1, N + 1), dtype=dt)
+        mlog = dt(0)
+        for g in range(nc):
+            M = Gam * phic[g] + np.diag(np.array([own_phi_common[a][g] for a in range(P)], dtype=dt))
+            Minv, ld, ok = _gauss_jordan(M)
+            if not ok:
+                return -np.inf
+            mlog += ld
+            ix = np.arange(P) * nc + g
+            Sc[np.ix_(ix, ix)] += Minv
+        for a, (SG, dG, rho) in enumerate(keeps):
+            s = slice(a * nc, (a + 1) * nc)
+            Sc[s, s] += SG
+            Sc[s, N] = dG
+            Sc[N, s] = dG
+            Sc[N, N] += rho
+        d, A = ldl_blocked(Sc, N, bs=64)
+        if not np.all(d > 0):
+            return -np.inf
+        return local - (np.sum(np.log(d)) + A[N, N] + mlog) / 2
+
+
+def _gauss_jordan(M):
+    """M^-1 and log|M| by in-place Gauss-Jordan without pivoting
+    (`common_minv_reg_kernel`)."""
+    M = M.copy()
+    n = M.shape[0]
+    ld = M.dtype.type(0)
+    ok = True
+    for k in range(n):
+        piv = M[k, k]
+        ok &= bool(piv > 0)
+        ld += np.log(piv) if piv > 0 else 0
+        pinv = 1 / piv
+        colk = M[:, k].copy()
+        rowk = M[k, :] * pinv
+        M -= np.outer(colk, rowk)
+        M[k, :] = rowk
+        M[:, k] = -colk * pinv
+        M[k, k] = pinv
+    return M, ld, ok

@@ -11,56 +11,88 @@ REF_EXAMPLES = os.path.join(GOLDEN, "ref_examples")
 sys.path.insert(0, ROOT)
 
 # Parity tolerance of the north star (BASELINE.json): 1e-6 absolute / 1e-10
-# relative in lnL.  For samples whose Sigma is numerically near-singular
-# (smallest eigenvalue of the unit-diagonal-scaled Sigma = lam), two correct
-# fp64 Cholesky orderings differ by ~ eps / lam relative, so the bound is
-# widened to COND_K * eps / lam * |lnL| there (documented in DESIGN.md).
+# relative in lnL ("strict").  Near-truth samples (where samplers spend their
+# time) are held to strict.  On prior draws the golden fixtures carry a
+# MEASURED per-sample spread: the largest pairwise difference between the
+# enterprise-order oracle, the device-order fp64 restatement and the device-
+# order extended-precision value (oracle/device_order_ref.py,
+# tests/golden/make_golden.py).  Two correct fp64 orderings of the same
+# likelihood really are that far apart there, so such samples are held to
+# max(strict, SPREAD_K * spread).  DESIGN.md §6.
 ATOL, RTOL = 1e-6, 1e-10
-COND_K = 64.0
-EPS = np.finfo(float).eps
+SPREAD_K = 4.0
 
 
 def pytest_configure(config):
     config.addinivalue_line("markers", "gpu: needs an MI355X (HIP device) and libewarp_hip.so")
+    config.addinivalue_line("markers", "gpu_ab: kernel A/B variants (dev library libewarp_hip_ab.so, "
+                                       "`make -C enterprise_warp_amd/csrc ab`); not part of the driver's -m gpu suite")
 
 
-def lnl_tolerance(ref, min_eig=None):
-    ref = np.asarray(ref, dtype=float)
-    tol = ATOL + RTOL * np.abs(ref)
-    if min_eig is not None:
-        lam = np.maximum(np.abs(np.asarray(min_eig, dtype=float)), 1e-300)
-        tol = np.maximum(tol, COND_K * EPS / lam * np.abs(ref))
+def pytest_collection_modifyitems(config, items):
+    skip = pytest.mark.skip(reason="A/B variant tests need a GPU and the dev library (make ab)")
+    for it in items:
+        if "gpu_ab" in it.keywords and not gpu_available():
+            it.add_marker(skip)
+
+
+def strict_tolerance(ref):
+    return ATOL + RTOL * np.abs(np.asarray(ref, dtype=float))
+
+
+def lnl_tolerance(ref, spread=None, near=None):
+    """strict; or max(strict, SPREAD_K * spread) on samples that are not
+    near-truth (`near` False) when a measured spread is given."""
+    tol = strict_tolerance(ref)
+    if spread is not None:
+        wide = np.maximum(tol, SPREAD_K * np.asarray(spread, dtype=float))
+        tol = wide if near is None else np.where(np.asarray(near, bool), tol, wide)
     return tol
 
 
-def oracle_lnl_cond(pta, X):
-    """Oracle lnL per sample and the sample's conditioning (min over pulsars
-    of the smallest eigenvalue of the unit-diagonal-scaled Sigma), as the
-    golden fixtures store it (tests/golden/make_golden.py)."""
+def check_parity(got, want, label, spread=None, near=None):
+    """GPU lnL vs a reference: no NaN, every non-finite value exactly -inf and
+    exactly where the reference is -inf, finite values within lnl_tolerance.
+    Prints max err / strict tolerance.  Returns that ratio."""
+    got = np.asarray(got, dtype=float)
+    want = np.asarray(want, dtype=float)
+    assert not np.isnan(got).any(), f"{label}: NaN in GPU lnL at {np.flatnonzero(np.isnan(got))}"
+    bad_inf = ~np.isfinite(got) & (got != -np.inf)
+    assert not bad_inf.any(), f"{label}: non-finite values other than -inf at {np.flatnonzero(bad_inf)}"
+    fin_g, fin_w = np.isfinite(got), np.isfinite(want)
+    assert np.array_equal(fin_g, fin_w), \
+        f"{label}: -inf pattern differs (gpu -inf at {np.flatnonzero(~fin_g)}, ref -inf at {np.flatnonzero(~fin_w)})"
+    if not fin_w.any():
+        return 0.0
+    err = np.abs(got[fin_w] - want[fin_w])
+    tol = lnl_tolerance(want[fin_w], None if spread is None else np.asarray(spread)[fin_w],
+                        None if near is None else np.asarray(near)[fin_w])
+    ratio = err / strict_tolerance(want[fin_w])
+    print(f"{label}: max err/strict {ratio.max():.3e}, max err/tol {np.max(err / tol):.3e} over {fin_w.sum()} samples")
+    ok = err <= tol
+    k = int(np.argmax(err / tol))
+    assert ok.all(), f"{label}: {(~ok).sum()} samples outside tolerance; worst sample {np.flatnonzero(fin_w)[k]}: " \
+                     f"err {err[k]:.3e} > tol {tol[k]:.3e}"
+    return float(ratio.max())
+
+
+def oracle_lnl(pta, X):
+    """Enterprise-order oracle lnL of every row of X."""
     from oracle.enterprise_ref import OraclePTA
     const = pta.constant_values()
     fixed = const if pta.white_fixed() else None
     o = OraclePTA([c.psr for c in pta.signal_collections], pta.oracle_terms(), fixed_params=fixed)
-    out, cond = [], []
+    out = []
     for x in X:
         d = dict(const)
         d.update(pta.map_params(x))
         out.append(o.lnlikelihood(d))
-        if o.correlated():
-            cond.append(correlated_min_eig(o, d))
-            continue
-        mins = []
-        for i, pp in enumerate(o.pulsars):
-            TNT = o.fixed[i][0] if o.fixed is not None else pp.white_terms(d)[0]
-            S = TNT + np.diag(1.0 / pp.phi(d))
-            sc = 1.0 / np.sqrt(np.diag(S))
-            mins.append(np.linalg.eigvalsh(S * sc[:, None] * sc[None, :])[0])
-        cond.append(min(mins))
-    return np.array(out), np.array(cond)
+    return np.array(out)
 
 
-def load_golden(name):
-    """Rebuild (pta, theta, lnl, min_eig) from a committed fixture."""
+def load_golden(name, full=False):
+    """Rebuild (pta, theta, lnl, min_eig) from a committed fixture; full=True
+    returns (pta, z) with every stored array (lnl_dev, lnl_exact, spread, near)."""
     from enterprise_warp_amd import synth
     from enterprise_warp_amd.pulsar import Pulsar
     z = np.load(os.path.join(GOLDEN, name + ".npz"), allow_pickle=False)
@@ -73,11 +105,13 @@ def load_golden(name):
     ns = synth.params_namespace(rec["Tspan"], rec["fixed_white"])
     pta = synth.build_pta(psrs, rec["per_psr_terms"], rec["common_terms"], ns, rec["noisedict"] or None)
     assert pta.param_names == rec["param_names"]
+    if full:
+        return pta, {k: z[k] for k in ("theta", "lnl", "lnl_dev", "lnl_exact", "spread", "near", "min_eig")}
     return pta, z["theta"], z["lnl"], z["min_eig"]
 
 
-GOLDEN_NAMES = ["c1_j1832", "c1_turnover", "c2_small", "c2_chromvary", "c3_small", "c3_freesp", "c4_small",
-                "c5_small", "c5_mono"]
+GOLDEN_NAMES = ["c1_j1832", "c1_turnover", "c1_system", "c2_small", "c2_chromvary", "c3_small", "c3_freesp",
+                "c4_small", "c5_small", "c5_mono", "c5_noauto", "c5_dipo"]
 
 
 def gpu_available():
@@ -92,15 +126,3 @@ def gpu_available():
 def require_gpu():
     if not gpu_available():
         pytest.fail("this test needs a HIP GPU (run with -m 'not gpu' on CPU-only hosts)")
-
-
-def correlated_min_eig(o, d):
-    """lambda_min of the unit-diagonal-scaled global Sigma = blockdiag(TNT) +
-    Phi^-1 of a correlated PTA (the conditioning of its one factorisation)."""
-    terms = [o.fixed[i] if o.fixed is not None else pp.white_terms(d) for i, pp in enumerate(o.pulsars)]
-    Phi, off = o.phi_global(d)
-    S, _ = o.phiinv_cliques(Phi)
-    for a, t in enumerate(terms):
-        S[off[a]:off[a + 1], off[a]:off[a + 1]] += t[0]
-    sc = 1.0 / np.sqrt(np.abs(np.diag(S)))
-    return np.linalg.eigvalsh(S * sc[:, None] * sc[None, :])[0]

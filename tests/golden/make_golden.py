@@ -23,47 +23,53 @@ ROOT = os.path.dirname(os.path.dirname(HERE))
 sys.path.insert(0, ROOT)
 
 from enterprise_warp_amd import synth  # noqa: E402
+from oracle.device_order_ref import DeviceOrderPTA  # noqa: E402
 from oracle.enterprise_ref import OraclePTA  # noqa: E402
 
 
+ORDERINGS = ("enterprise", "device", "device_blas", "reverse_chol", "extended")
+
+
 def oracle_lnl(pta, X):
-    """lnL per sample and the sample's conditioning: min over pulsars of the
-    smallest eigenvalue of the unit-diagonal-scaled Sigma (near 0 = the
-    Cholesky-failure boundary, where -inf parity is inherently fragile)."""
+    """Per sample, the lnL of five correct orderings of the same likelihood:
+      enterprise    oracle/enterprise_ref.py (the full Sigma by cho_factor)
+      device        the device's order (oracle/device_order_ref.py: the
+                    contraction kernels' FMA accumulation order for the Gram,
+                    schur_kernel's timing-model elimination, blocked LDL^T)
+      device_blas   the same with a BLAS Gram and a plain Schur step
+      reverse_chol  the Gram summed over the TOAs in reverse, unblocked Cholesky
+      extended      the device order in x87 extended precision (eps 1.1e-19):
+                    a near-exact value for the same fp64 inputs
+    and the measured spread = max - min of the five (0 where all are -inf; inf
+    where they disagree on -inf).  The GPU tests bound |gpu - ref| by
+    max(strict, 4 spread) (strict = 1e-6 + 1e-10 |lnL|, BASELINE.json) on
+    prior draws and by strict on near-truth draws.  Also returns the
+    conditioning of what the device factors (informational)."""
     const = pta.constant_values()
     fixed = const if pta.white_fixed() else None
-    o = OraclePTA([c.psr for c in pta.signal_collections], pta.oracle_terms(), fixed_params=fixed)
-    out, cond = [], []
-    for x in X:
+    psrs = [c.psr for c in pta.signal_collections]
+    terms = pta.oracle_terms()
+    models = [OraclePTA(psrs, terms, fixed_params=fixed),
+              DeviceOrderPTA(psrs, terms, fixed, np.float64, gram_mode="device"),
+              DeviceOrderPTA(psrs, terms, fixed, np.float64, gram_mode="blas"),
+              DeviceOrderPTA(psrs, terms, fixed, np.float64, gram_mode="reverse", factor="chol"),
+              DeviceOrderPTA(psrs, terms, fixed, np.longdouble)]
+    vals = np.zeros((len(models), len(X)))
+    cond = []
+    for j, x in enumerate(X):
         d = dict(const)
         d.update(pta.map_params(x))
-        out.append(o.lnlikelihood(d))
-        if o.correlated():
-            cond.append(correlated_min_eig(o, d))
-            continue
-        mins = []
-        for i, pp in enumerate(o.pulsars):
-            TNT = o.fixed[i][0] if fixed is not None else pp.white_terms(d)[0]
-            S = TNT + np.diag(1.0 / pp.phi(d))
-            sc = 1.0 / np.sqrt(np.diag(S))
-            mins.append(np.linalg.eigvalsh(S * sc[:, None] * sc[None, :])[0])
-        cond.append(min(mins))
-    return np.array(out), np.array(cond)
+        for i, mdl in enumerate(models):
+            vals[i, j] = mdl.lnlikelihood(d)
+        cond.append(models[2].min_eig(d))
+    fin = np.isfinite(vals).all(axis=0)
+    spread = np.zeros(len(X))
+    spread[fin] = vals[:, fin].max(axis=0) - vals[:, fin].min(axis=0)
+    spread[~fin & np.isfinite(vals).any(axis=0)] = np.inf     # orderings disagree on -inf
+    return vals, spread, np.array(cond)
 
 
-def correlated_min_eig(o, d):
-    """lambda_min of the unit-diagonal-scaled global Sigma = blockdiag(TNT) +
-    Phi^-1 of a correlated PTA (the conditioning of its one factorisation)."""
-    terms = [o.fixed[i] if o.fixed is not None else pp.white_terms(d) for i, pp in enumerate(o.pulsars)]
-    Phi, off = o.phi_global(d)
-    S, _ = o.phiinv_cliques(Phi)
-    for a, t in enumerate(terms):
-        S[off[a]:off[a + 1], off[a]:off[a + 1]] += t[0]
-    sc = 1.0 / np.sqrt(np.abs(np.diag(S)))
-    return np.linalg.eigvalsh(S * sc[:, None] * sc[None, :])[0]
-
-
-def dump(name, pta, recipe, X):
+def dump(name, pta, recipe, X, n_prior=8):
     psrs = [c.psr for c in pta.signal_collections]
     arrays = {}
     for i, p in enumerate(psrs):
@@ -77,11 +83,17 @@ def dump(name, pta, recipe, X):
             arrays[f"p{i}_flag_{k}"] = v.astype(str)
     recipe = dict(recipe, names=[p.name for p in psrs], flag_names=[sorted(p.flags) for p in psrs],
                   param_names=pta.param_names)
-    lnl, cond = oracle_lnl(pta, X)
+    vals, spread, cond = oracle_lnl(pta, X)
+    lnl, dev, ex = vals[0], vals[1], vals[-1]
+    near = np.arange(len(X)) >= n_prior          # rows [n_prior:) are near-truth draws
     np.savez_compressed(os.path.join(HERE, name + ".npz"), recipe=np.array(json.dumps(recipe)), theta=X, lnl=lnl,
-                        min_eig=cond, **arrays)
-    print(name, "n_psr", len(psrs), "nparam", X.shape[1], "n_inf", int(np.sum(~np.isfinite(lnl))),
-          "min_eig", np.round(np.log10(np.abs(cond)), 1))
+                        lnl_dev=dev, lnl_exact=ex, lnl_orderings=vals, orderings=np.array(ORDERINGS),
+                        spread=spread, near=near, min_eig=cond, **arrays)
+    strict = 1e-6 + 1e-10 * np.abs(ex)
+    with np.errstate(invalid="ignore", divide="ignore"):
+        print(name, "n_psr", len(psrs), "nparam", X.shape[1], "n_inf", int(np.sum(~np.isfinite(lnl))),
+              "spread/strict", np.array2string(spread / strict, precision=1, max_line_width=200),
+              "log10 min_eig", np.round(np.log10(np.abs(cond)), 1))
 
 
 def recipe_of(cfg, per_psr, common, fixed_white):
@@ -163,10 +175,32 @@ def main():
                                  "fixed_white": False, "noisedict": {}}, X)
     # c5 small: fixed white noise + ECORR, Hellings-Downs correlated common
     # process (cross-pulsar Sigma), and the same model with a monopole ORF
-    for name, gwb in (("c5_small", "hd_vary_gamma_5_nfreqs"), ("c5_mono", "mono_vary_gamma_4_nfreqs")):
+    for name, gwb in (("c5_small", "hd_vary_gamma_5_nfreqs"), ("c5_mono", "mono_vary_gamma_4_nfreqs"),
+                      ("c5_noauto", "hd_noauto_vary_gamma_5_nfreqs"), ("c5_dipo", "dipo_vary_gamma_4_nfreqs")):
         c5 = synth.config_c5(n_psr=4, n_toa=500, seed=50, epoch_size=4, gwb=gwb, nfreqs=10)
-        X = np.vstack([synth.prior_draws(c5.pta, 8, 51), synth.near_draws(c5.pta, c5.truth, 8, 52)])
+        truth = dict(c5.truth)
+        if "noauto" in gwb:
+            # Gamma without auto terms: M_g = diag(phi_red) + Gamma_off phi_gw is
+            # positive definite only while the pulsars' own red noise dominates
+            truth["gw_log10_A"] = -15.5
+        X = np.vstack([synth.prior_draws(c5.pta, 8, 51), synth.near_draws(c5.pta, truth, 8, 52)])
         dump(name, c5.pta, recipe_of(c5, c5.terms, c5.common, True), X)
+    # c1 system noise: the reference's system_noise_example.dat /
+    # system_noise_example.json for J1832-0836 (efac / equad fixed from the
+    # example noise file; spin + DM noise; system noise on the PDFB_40CM and
+    # CASPSR_40CM groups; band noise on 10CM: enterprise_models.py:256-338)
+    c1s = synth.config_c1(os.path.join(HERE, "ref_examples"))
+    psr = c1s.pta.signal_collections[0].psr
+    ns = synth.params_namespace(np.ptp(psr.toas), True)
+    terms_s = {"efac": "by_backend", "equad": "by_backend", "spin_noise": "powerlaw", "dm_noise": "powerlaw",
+               "system_noise": ["PDFB_40CM", "CASPSR_40CM"], "ppta_band_noise": ["10CM"]}
+    wn = {k: v for k, v in c1s.truth.items() if k.endswith("_efac") or k.endswith("_log10_tnequad")}
+    pta_s = synth.build_pta([psr], terms_s, {}, ns, wn)
+    truth_s = synth.truth_values(pta_s, 8, white=wn)
+    synth.simulate_residuals(pta_s, truth_s, 9)
+    X = np.vstack([synth.prior_draws(pta_s, 8, 19), synth.near_draws(pta_s, truth_s, 8, 20)])
+    dump("c1_system", pta_s, {"per_psr_terms": terms_s, "common_terms": {}, "Tspan": float(np.ptp(psr.toas)),
+                              "fixed_white": True, "noisedict": wn}, X)
 
 
 if __name__ == "__main__":

@@ -3,7 +3,7 @@ would take minutes, checked through size-independent identities."""
 import numpy as np
 import pytest
 
-from conftest import lnl_tolerance
+from conftest import check_parity
 from enterprise_warp_amd import sharding, synth
 
 pytestmark = pytest.mark.gpu
@@ -48,7 +48,7 @@ def test_c3_mfma_vs_lds_full_size(require_gpu, c3):
     pta.engine().set_kernel_mode(1)
     b = pta.get_lnlikelihood_batch(X)
     pta.engine().set_kernel_mode(0)
-    assert np.all(np.abs(a - b) <= lnl_tolerance(b))
+    check_parity(a, b, "C3 mfma vs lds")
 
 
 def test_c3_pulsar_permutation_invariance(require_gpu, c3):
@@ -60,28 +60,63 @@ def test_c3_pulsar_permutation_invariance(require_gpu, c3):
     a = pta.get_lnlikelihood_batch(X)
     rev = PTA(list(reversed(pta.signal_collections)))
     b = rev.get_lnlikelihood_batch(X)
-    assert np.all(np.abs(a - b) <= lnl_tolerance(a))
+    check_parity(b, a, "C3 reversed pulsars")
 
 
-@pytest.mark.parametrize("mode", [0, 2, 3, 4, 5, 6, 8, 9, 10, 11, 12, 13])
-def test_c3_chol_variants_vs_oracle(require_gpu, c3, mode):
-    """Every register-blocked Cholesky variant (Cholesky / LDL^T panel, looped
-    / unrolled, 1-2 waves per SIMD) against the oracle on full-size C3: near-
-    truth draws at the strict bound, prior draws (loud red noise, Sigma close
-    to singular) at the conditioning-widened bound of conftest.lnl_tolerance."""
-    from conftest import oracle_lnl_cond
+@pytest.mark.parametrize("mode", [0, 2])
+def test_c3_chol_vs_oracle(require_gpu, c3, mode):
+    """The default register-blocked factorisation (mode 0: blocked LDL^T
+    panel) and the round-1 Cholesky panel (mode 2) against the oracle on
+    full-size C3 near-truth draws, strict bound."""
+    from conftest import oracle_lnl
     pta = c3.pta
-    X = np.concatenate([synth.near_draws(pta, c3.truth, 16, 7), synth.prior_draws(pta, 16, 8)])
+    X = synth.near_draws(pta, c3.truth, 16, 7)
     pta.engine().set_kernel_mode(mode)
     try:
         got = pta.get_lnlikelihood_batch(X)
     finally:
         pta.engine().set_kernel_mode(0)
-    want, cond = oracle_lnl_cond(pta, X)
-    fin = np.isfinite(want)
-    strict = np.arange(len(X)) < 16
-    err = np.abs(got - want)
-    assert np.all(err[strict] <= lnl_tolerance(want[strict])), f"mode {mode}: near-truth worst {err[strict].max():.3e}"
-    tol = lnl_tolerance(want[fin], cond[fin])
-    assert np.all(err[fin] <= tol), f"mode {mode}: worst err/tol {np.max(err[fin] / tol):.3e}"
-    assert np.array_equal(np.isfinite(got), fin)
+    check_parity(got, oracle_lnl(pta, X), f"C3 mode {mode}")
+
+
+@pytest.mark.parametrize("name", ["c3_small", "c2_small", "c5_small", "c4_small"])
+def test_multi_context_handle_is_bit_identical(require_gpu, name):
+    """ewh_create with a device list: the batch is split over the contexts
+    (units by cost for uncorrelated / CURN models, samples for a correlated
+    common process) and must give the single-context result bit for bit.
+    On the one-GPU box the list [0, 0] (two replicas on one device) and
+    [0, 0, 0] exercise the split; a node passes [0..7]."""
+    from conftest import load_golden
+    pta, X, _, _ = load_golden(name)
+    X = np.vstack([X] * 8)                         # 128 samples: ranges split pulsars mid-row
+    one = pta.get_lnlikelihood_batch(X)
+    terms1 = pta.engine().unit_terms(len(X))
+    for devs in ([0, 0], [0, 0, 0]):
+        eng = pta.engine(devices=devs)
+        assert eng.num_devices() == len(devs)
+        got = pta.get_lnlikelihood_batch(X)
+        np.testing.assert_array_equal(got, one)
+        np.testing.assert_array_equal(eng.unit_terms(len(X)), terms1)
+    pta.engine(devices=[0])
+
+
+def test_set_fixed_white_in_place(require_gpu):
+    """pta.set_default_params(new white-noise constants) (enterprise_warp.py:
+    504-508) updates the cached TNT in place (ewh_set_fixed_white, same
+    handle) and equals a PTA built from scratch with those constants."""
+    from conftest import check_parity, load_golden, oracle_lnl
+    pta, X, lnl, _ = load_golden("c3_small")
+    eng = pta.engine()
+    before = pta.get_lnlikelihood_batch(X)
+    const = pta.constant_values()
+    rng = np.random.default_rng(5)
+    new = {k: (v * rng.uniform(0.95, 1.05) if k.endswith("_efac") else v + rng.uniform(-0.2, 0.2))
+           for k, v in const.items() if k.endswith(("_efac", "_log10_tnequad", "_log10_ecorr"))}
+    pta.set_default_params(new)
+    assert pta.engine() is eng                      # no rebuild
+    got = pta.get_lnlikelihood_batch(X)
+    assert not np.array_equal(got, before)
+    fresh, _, _, _ = load_golden("c3_small")
+    fresh.set_default_params(new)
+    np.testing.assert_array_equal(fresh.get_lnlikelihood_batch(X), got)
+    check_parity(got[8:], oracle_lnl(pta, X[8:]), "c3_small new white noise")

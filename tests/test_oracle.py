@@ -178,3 +178,58 @@ def test_correlated_reduces_to_curn_without_cross_terms():
             g.pop("orf", None)
     curn = o.lnlikelihood(c.truth)
     assert abs(corr - curn) <= 1e-10 * abs(curn)
+
+
+# --------------------------------------------------------------------------
+# device-order restatement (oracle/device_order_ref.py)
+# --------------------------------------------------------------------------
+@pytest.mark.parametrize("name", GOLDEN_NAMES)
+def test_device_order_matches_enterprise_order_near_truth(name):
+    """The device's ordering (timing model eliminated once, r as the last
+    column, blocked LDL^T; correlated: partial factorisations + M_g^-1 +
+    dense Sigma_c) is the same likelihood: on every near-truth golden sample
+    its fp64 and extended-precision values agree with the enterprise-order
+    oracle at the strict bound; the -inf pattern is identical everywhere."""
+    from conftest import strict_tolerance
+    pta, z = load_golden(name, full=True)
+    near = z["near"]
+    for key in ("lnl_dev", "lnl_exact"):
+        assert np.array_equal(np.isfinite(z[key]), np.isfinite(z["lnl"]))
+        fin = near & np.isfinite(z["lnl"])
+        assert np.all(np.abs(z[key][fin] - z["lnl"][fin]) <= strict_tolerance(z["lnl"][fin])), key
+    assert np.all(z["spread"][np.isfinite(z["lnl"])] >= 0)
+
+
+@pytest.mark.parametrize("name", GOLDEN_NAMES)
+def test_device_order_reproduces_golden(name):
+    """DeviceOrderPTA (fp64, the device's accumulation order) regenerates the
+    stored lnl_dev bit for bit; the extended-precision form regenerates
+    lnl_exact on two samples."""
+    from oracle.device_order_ref import DeviceOrderPTA
+    pta, z = load_golden(name, full=True)
+    const_ = pta.constant_values()
+    fixed = const_ if pta.white_fixed() else None
+    psrs = [c.psr for c in pta.signal_collections]
+    d64 = DeviceOrderPTA(psrs, pta.oracle_terms(), fixed, np.float64, gram_mode="device")
+    dld = DeviceOrderPTA(psrs, pta.oracle_terms(), fixed, np.longdouble)
+    rows = range(len(z["theta"])) if fixed is not None else range(0, len(z["theta"]), 4)   # (varying WN: slow)
+    for i in rows:
+        x = z["theta"][i]
+        d = dict(const_)
+        d.update(pta.map_params(x))
+        got = d64.lnlikelihood(d)
+        want = z["lnl_dev"][i]
+        assert got == want or (not np.isfinite(want) and got == want)
+        if i in (0, 8):
+            assert dld.lnlikelihood(d) == z["lnl_exact"][i]
+
+
+def test_device_order_extended_precision_is_closer_on_ill_conditioned_draws():
+    """Where the two fp64 orderings drift apart (large spread), the extended-
+    precision value sits within that spread of both: the spread measures fp64
+    rounding of an ill-conditioned factorisation, not a model difference."""
+    pta, z = load_golden("c2_small", full=True)
+    i = int(np.argmax(z["spread"]))
+    assert z["spread"][i] > 1e-4                      # c2_small sample 1: a near-singular prior draw
+    lo, hi = min(z["lnl"][i], z["lnl_dev"][i]), max(z["lnl"][i], z["lnl_dev"][i])
+    assert lo - z["spread"][i] <= z["lnl_exact"][i] <= hi + z["spread"][i]
