@@ -85,6 +85,24 @@ class HyperModel:
         lp[(ks < 0) | (ks >= self.num_models)] = -np.inf
         return lp
 
+    @property
+    def pulsars(self):
+        out = []
+        for m in self.models.values():
+            for p in getattr(m, "pulsars", []):
+                if p not in out:
+                    out.append(p)
+        return out
+
+    def setup_sampler(self, outdir="chains", resume=False, sample_nmodel=True, empirical_distr=None, groups=None,
+                      human=None, loglkwargs=None, logpkwargs=None, seed=None):
+        """enterprise_extensions HyperModel.setup_sampler (run_example_paramfile.py:33):
+        the PTMCMC sampler over the union parameters + nmodel, with a prior-draw
+        jump on nmodel (enterprise_warp_amd.ptmcmc)."""
+        from .ptmcmc import setup_sampler
+        return setup_sampler(self, outdir=outdir, resume=resume, empirical_distr=empirical_distr, groups=groups,
+                             human=human, loglkwargs=loglkwargs, logpkwargs=logpkwargs, seed=seed)
+
     def initial_sample(self, rng=None):
         rng = np.random.default_rng(rng)
         x = np.empty(len(self.param_names))

@@ -3,11 +3,15 @@ the MI355X likelihood.
 
     python -m enterprise_warp_amd.run --prfile params.dat [--num N] [--niter K] [--nchains B]
 
-Params -> init_pta (one PTA per `{N}` model block) -> one PTA or, for several
-blocks, the HyperModel (run_example_paramfile.py:25-45) -> the batched
-Metropolis sampler (PTMCMCSampler and bilby are not installed; the chains go
-to the paramfile's output directory as chain_1.txt with pars.txt beside it).
+Params -> init_pta (one PTA per `{N}` model block) -> for `sampler:
+ptmcmcsampler` the reference's PTMCMC branch (run_example_paramfile.py:25-45:
+model_utils.setup_sampler / HyperModel.setup_sampler, x0 from the priors,
+sampler.sample(x0, nsamp, **sampler kwargs that sample() takes), one theta
+per device call); otherwise, or with --batched, the batched Metropolis
+sampler (B chains per device call; bilby is not installed).  Chains go to the
+paramfile's output directory as chain_1.txt with pars.txt beside it.
 """
+import inspect
 import optparse
 import os
 import sys
@@ -33,6 +37,7 @@ def parse_commandline(argv=None):
     p.add_option("--niter", type=int, default=None, help="iterations (default: the paramfile's nsamp)")
     p.add_option("--nchains", type=int, default=256, help="chains evaluated per device call")
     p.add_option("--seed", type=int, default=0)
+    p.add_option("--batched", action="store_true", help="batched Metropolis even for sampler: ptmcmcsampler")
     opts, _ = p.parse_args(argv)
     return opts
 
@@ -58,6 +63,22 @@ def main(argv=None):
         if all(n in df.index for n in names):
             cov = df.loc[names, names].to_numpy()
     niter = eo.niter if eo.niter is not None else int(getattr(params, "nsamp", 1000))
+    if getattr(params, "sampler", "") == "ptmcmcsampler" and not eo.batched:
+        # the reference's PTMCMC branch, call for call
+        from . import model_utils
+        if len(ptas) == 1:
+            sampler = model_utils.setup_sampler(ptas[0], resume=False, outdir=outdir or "chains", seed=eo.seed)
+            x0 = np.hstack([np.atleast_1d(p.sample()) for p in ptas[0].params])
+        else:
+            sampler = model.setup_sampler(resume=False, outdir=outdir or "chains", seed=eo.seed)
+            x0 = model.initial_sample()
+        accepted = inspect.getfullargspec(sampler.sample).args
+        kw = {k: v for k, v in params.sampler_kwargs.items() if k in accepted and k not in ("Niter", "p0")}
+        x = sampler.sample(x0, niter, **kw)
+        like = model.get_lnlikelihood(x)
+        post = like + model.get_lnprior(x)
+        print(f"{niter} PTMCMC iterations; acceptance {sampler.acceptance_rate:.3f}; final ln posterior {post:.6f}")
+        return x[None, :], np.array([post]), np.array([like])
     sampler = BatchedMH(model, nchains=eo.nchains, outdir=outdir, seed=eo.seed, cov=cov)
     X, post, like = sampler.sample(niter=niter)
     best = int(np.argmax(post))

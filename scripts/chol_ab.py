@@ -2,6 +2,10 @@
 (one process, R rounds, median and min per variant; guide §5.4 rule 24).
 
     python scripts/chol_ab.py [--rounds 7] [--modes 0,2,1]
+
+Modes 3-6 and 8-13 live in the dev library only (make -C
+enterprise_warp_amd/csrc dev); this script loads it unless EWARP_HIP_LIB
+names another build.
 """
 import argparse
 import json
@@ -10,7 +14,9 @@ import sys
 
 import numpy as np
 
-sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, ROOT)
+os.environ.setdefault("EWARP_HIP_LIB", os.path.join(ROOT, "enterprise_warp_amd", "libewarp_hip_dev.so"))
 
 
 def main():

@@ -1,13 +1,10 @@
 #!/bin/bash
-# GPU tests, C3 Cholesky A/B, per-config timings (C2/C3/C4), bench line.
+# One GPU session: GPU tests (verbose), smoke, bench (with CPU baseline + sampler latency).
 set -u
 cd "${GRAFT_REPO_ROOT:-/root/repo}"; mkdir -p gpurun_out; export TMPDIR=/tmp
-MODES=${1:-0,9}
-step() { local name=$1 secs=$2; shift 2
-  timeout -k 10 "$secs" "$@" > "gpurun_out/$name.log" 2>&1; local rc=$?
-  echo "== $name rc=$rc"; grep -v "amdgpu.ids" "gpurun_out/$name.log" | tail -3 | cut -c1-300
-  case $rc in 0|1|5) ;; *) echo "stopping after $name"; exit $rc;; esac; }
-step pytest_gpu 900 python -u -m pytest tests -x -q -m gpu --timeout 300 --timeout-method thread
-step chol_ab 400 python scripts/chol_ab.py --rounds 5 --modes $MODES
-step configs 400 python scripts/bench_configs.py --configs c2,c3,c4 --reps 3 --check 2
-step bench 400 python bench.py --steps 20 --warmup 3 --cpu-seconds 10
+timeout -k 10 1100 python -u -m pytest tests -v -s -m gpu --timeout 400 --timeout-method thread > gpurun_out/pytest_gpu.log 2>&1; rc=$?
+echo pytest rc=$rc; grep -E "passed|failed|FAILED|^E  " gpurun_out/pytest_gpu.log | tail -30
+case $rc in 0|1) ;; *) exit $rc;; esac
+timeout -k 10 400 python __graft_entry__.py smoke > gpurun_out/smoke.log 2>&1; rc=$?; echo smoke rc=$rc; tail -2 gpurun_out/smoke.log
+case $rc in 0|1) ;; *) exit $rc;; esac
+timeout -k 10 600 python bench.py > gpurun_out/bench.log 2>&1; echo bench rc=$?; tail -1 gpurun_out/bench.log

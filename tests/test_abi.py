@@ -71,3 +71,15 @@ def test_engine_fails_loudly_without_gpu():
     with pytest.raises(_lib.EngineError):
         pta.get_lnlikelihood_batch(X[:2])
     assert np.isfinite(X).all()
+
+
+def test_dev_exports_only_in_dev_library():
+    """The kernel A/B variants and diagnostic exports are not in the product
+    library (enterprise_warp_amd/csrc/Makefile `dev`)."""
+    out = subprocess.run(["nm", "-D", "--defined-only", _lib.LIB_PATH], capture_output=True, text=True).stdout
+    for name in _lib.DEV_EXPORTS:
+        assert name not in out
+    if os.path.exists(_lib.DEV_LIB_PATH):
+        out = subprocess.run(["nm", "-D", "--defined-only", _lib.DEV_LIB_PATH], capture_output=True, text=True).stdout
+        for name in _lib.DEV_EXPORTS + _lib.EXPORTS:
+            assert re.search(rf"\bT {name}\b", out), name

@@ -1,0 +1,23 @@
+"""Kernel A/B variants (dev library libewarp_hip_dev.so; marker gpu_ab, not
+part of the driver's -m gpu suite): each variant against the oracle on
+full-size C3 at the strict bound, in a separate process (the dev library is
+a different build of the same ABI)."""
+import os
+import subprocess
+import sys
+
+import pytest
+
+from conftest import ROOT
+
+pytestmark = pytest.mark.gpu_ab
+
+
+def test_chol_variants_vs_oracle():
+    lib = os.path.join(ROOT, "enterprise_warp_amd", "libewarp_hip_dev.so")
+    if not os.path.exists(lib):
+        pytest.skip("dev library not built (make -C enterprise_warp_amd/csrc dev)")
+    r = subprocess.run([sys.executable, os.path.join(ROOT, "scripts", "check_variants.py")], capture_output=True,
+                       text=True, timeout=600)
+    print(r.stdout[-4000:], r.stderr[-2000:])
+    assert r.returncode == 0

@@ -129,7 +129,57 @@ def test_paramfile_driver_hypermodel(require_gpu, tmp_path, monkeypatch):
         shutil.copytree(f"{REF_EXAMPLES}/{d}", tmp_path / d)
     monkeypatch.chdir(tmp_path)
     X, post, like = run.main(["--prfile", "example_params/default_hypermodel.dat", "--niter", "30",
-                              "--nchains", "32", "--seed", "1"])
+                              "--nchains", "32", "--seed", "1", "--batched"])
     assert X.shape[0] == 32 and np.all(np.isfinite(post))
     out = list(tmp_path.glob("out/**/chain_1.txt"))
     assert len(out) == 1 and np.loadtxt(out[0]).shape[0] == 32 * 3
+
+
+def test_ptmcmc_driver_hypermodel(require_gpu, tmp_path, monkeypatch):
+    """The reference's PTMCMC branch (run_example_paramfile.py:31-45) on its
+    default_hypermodel.dat: HyperModel.setup_sampler, initial_sample,
+    sampler.sample(x0, N, **kwargs filtered by sample()'s signature), one
+    theta per device call.  Every logged state's ln likelihood is re-evaluated
+    by the oracle (the active model's PTA) at the strict bound."""
+    import shutil
+    from conftest import REF_EXAMPLES
+    from enterprise_warp_amd import run
+    for d in ("data", "example_params", "example_noisemodels", "example_noisefiles"):
+        shutil.copytree(f"{REF_EXAMPLES}/{d}", tmp_path / d)
+    monkeypatch.chdir(tmp_path)
+    from enterprise_warp_amd import warp
+    from enterprise_warp_amd.hypermodel import HyperModel
+    x, post, like = run.main(["--prfile", "example_params/default_hypermodel.dat", "--niter", "400", "--seed", "3"])
+    assert np.isfinite(post[0])
+    chain = np.loadtxt(next(tmp_path.glob("out/**/chain_1.txt")))
+    assert chain.shape == (40, x.shape[1] + 4)
+    hm = HyperModel(warp.init_pta(warp.Params("example_params/default_hypermodel.dat", opts=None)))
+    rows = chain[-8:]
+    want = []
+    for r in rows:
+        k = int(np.rint(r[hm._inm]))
+        sub = hm.models[k]
+        want.append(oracle_lnl(sub, r[hm._idx[k]][None, :])[0])
+    check_parity(rows[:, -3], np.array(want), "PTMCMC logged lnL")
+
+
+def test_c5_full_size_vs_oracle(require_gpu):
+    """BASELINE config 5 at its stated size (100 psr x 20k TOAs, HD GWB 14
+    freqs, dense 2801^2 Sigma_c per sample on the device): near-truth draws
+    against the enterprise-order oracle's dense 13,200^2 factorisation,
+    computed in the dev container (tests/golden/make_c5_full.py, values in
+    c5_full.json with a hash of the seeded synthetic arrays), strict bound."""
+    import json
+    import os
+    from conftest import GOLDEN
+    from golden.make_c5_full import synth_hash, synth_sums
+    with open(os.path.join(GOLDEN, "c5_full.json")) as fh:
+        rec = json.load(fh)
+    c5 = synth.config_c5()
+    assert synth_hash(c5.pta) == rec["synth_sha256"], "synthetic C5 differs from the one the oracle saw"
+    np.testing.assert_allclose(synth_sums(c5.pta), rec["synth_sums"], rtol=1e-9)
+    assert c5.pta.param_names == rec["param_names"]
+    X = np.array(rec["theta"])
+    got = c5.pta.get_lnlikelihood_batch(X)
+    check_parity(got, np.array(rec["lnl"]), "C5-full vs enterprise-order")
+    check_parity(got, np.array(rec["lnl_dev"]), "C5-full vs device-order fp64")
