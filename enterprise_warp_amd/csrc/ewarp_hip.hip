@@ -797,12 +797,29 @@ struct DevCtx {
   int cchunk_cap = 0;         // samples the dense Sigma_c budget allows per chunk
   int n_param_desc = 0;
   bool osmode = false;        // EWH_COMMON_OPTSTAT handle (ewh_optstat only)
+  // captured ewh_lnl_batch sequences (H2D, launches, D2H) per batch size:
+  // a sampler's single-theta calls replay one graph instead of ~5 API calls
+  struct Graph {
+    int B, mode;
+    const void *ht, *ho;
+    hipGraphExec_t exec;
+    long long last_use;
+  };
+  std::vector<Graph> graphs;
+  long long graph_clock = 0;
 };
 
 namespace {
 
+// captured graphs hold device pointers: any (re)allocation invalidates them
+void drop_graphs(DevCtx* h) {
+  for (auto& g : h->graphs) (void)hipGraphExecDestroy(g.exec);
+  h->graphs.clear();
+}
+
 template <typename T>
 int dalloc(DevCtx* h, T** p, size_t count) {
+  drop_graphs(h);
   *p = nullptr;
   if (count == 0) count = 1;
   hipError_t e = hipMalloc((void**)p, count * sizeof(T));
@@ -1288,6 +1305,7 @@ void destroy_ctx(DevCtx* h) {
   if (!h) return;
   (void)hipSetDevice(h->device);
   if (h->stream) (void)hipStreamSynchronize(h->stream);
+  drop_graphs(h);
   for (void* p : h->allocs) (void)hipFree(p);
   if (h->stream) (void)hipStreamDestroy(h->stream);
   delete h;
@@ -1628,6 +1646,75 @@ int ensure_pinned(double** p, size_t* cap, size_t need) {
 
 }  // namespace
 
+namespace {
+
+// enqueue one single-context batch on h->stream: H2D of theta from the pinned
+// staging, the unit launches + reduction, D2H of lnL into the pinned staging
+int enqueue_single(ewh_handle* H, DevCtx* h, int B) {
+  const int np = H->n_param;
+  int rc;
+  if (np > 0)
+    EWH_HIP(hipMemcpyAsync(h->d_theta, H->h_theta, sizeof(double) * (size_t)B * np, hipMemcpyHostToDevice,
+                           h->stream));
+  if ((rc = ctx_units(h, h->d_theta, B, 0, (long long)H->P * B, h->d_out, h->stream, true))) return rc;
+  EWH_HIP(hipMemcpyAsync(H->h_out, h->d_out, sizeof(double) * B, hipMemcpyDeviceToHost, h->stream));
+  return 0;
+}
+
+constexpr size_t GRAPH_CACHE = 8;
+
+// One device: replay the captured graph of this batch size when there is one;
+// otherwise run the batch eagerly (that also sizes every scratch buffer) and
+// capture the same sequence for the next call.
+int lnl_batch_single(ewh_handle* H, DevCtx* h, int B, double* out_host) {
+  int rc;
+  EWH_HIP(hipSetDevice(h->device));
+  if ((rc = ensure_pinned(&H->h_out, &H->h_out_cap, (size_t)B))) return rc;
+  if ((rc = ensure_io(h, B))) return rc;
+  DevCtx::Graph* hit = nullptr;
+  for (auto& g : h->graphs)
+    if (g.B == B && g.mode == h->kernel_mode && g.ht == H->h_theta && g.ho == H->h_out) hit = &g;
+  if (hit) {
+    hit->last_use = ++h->graph_clock;
+    EWH_HIP(hipGraphLaunch(hit->exec, h->stream));
+  } else {
+    if ((rc = enqueue_single(H, h, B))) return rc;
+  }
+  EWH_HIP(hipStreamSynchronize(h->stream));
+  std::memcpy(out_host, H->h_out, sizeof(double) * B);
+  H->last_split.assign(1, {0, (long long)H->P * B});
+  H->last_B = B;
+  if (hit || h->corr) return 0;     // (correlated batches are long: launch overhead is immaterial)
+  // capture for the next call of this size (buffers are sized now, so the
+  // sequence makes no allocation or synchronous call)
+  hipGraph_t graph = nullptr;
+  hipGraphExec_t exec = nullptr;
+  if (hipStreamBeginCapture(h->stream, hipStreamCaptureModeThreadLocal) != hipSuccess) return 0;
+  rc = enqueue_single(H, h, B);
+  const hipError_t e = hipStreamEndCapture(h->stream, &graph);
+  if (rc || e != hipSuccess || !graph) {
+    if (graph) (void)hipGraphDestroy(graph);
+    (void)hipGetLastError();
+    return 0;                       // no graph: the eager path stays correct
+  }
+  const hipError_t ei = hipGraphInstantiate(&exec, graph, nullptr, nullptr, 0);
+  (void)hipGraphDestroy(graph);
+  if (ei != hipSuccess) {
+    (void)hipGetLastError();
+    return 0;
+  }
+  if (h->graphs.size() >= GRAPH_CACHE) {
+    auto lru = std::min_element(h->graphs.begin(), h->graphs.end(),
+                                [](const DevCtx::Graph& a, const DevCtx::Graph& b) { return a.last_use < b.last_use; });
+    (void)hipGraphExecDestroy(lru->exec);
+    h->graphs.erase(lru);
+  }
+  h->graphs.push_back({B, h->kernel_mode, H->h_theta, H->h_out, exec, ++h->graph_clock});
+  return 0;
+}
+
+}  // namespace
+
 extern "C" {
 
 int ewh_version(void) { return EWH_ABI_VERSION; }
@@ -1677,6 +1764,7 @@ int ewh_set_fixed_white(ewh_handle* H, const double* values) {
                                h->stream));
     }
     EWH_HIP(hipStreamSynchronize(h->stream));
+    drop_graphs(h);
     if (h->white_fixed) {
       int rc = setup_fixed(h);
       if (rc) return rc;
@@ -1689,7 +1777,11 @@ int ewh_set_kernel_mode(ewh_handle* H, int32_t mode) {
   if (!H || mode < 0 || mode > 13) return set_err(EWH_E_INVALID, "bad handle / mode");
   if (mode >= 3 && mode != 7 && !ab_variants_built())
     return set_err(EWH_E_UNSUPPORTED, "kernel A/B variants are built only into the dev library (make dev)");
-  for (DevCtx* h : H->ctx) h->kernel_mode = mode;
+  for (DevCtx* h : H->ctx) {
+    h->kernel_mode = mode;
+    (void)hipSetDevice(h->device);
+    drop_graphs(h);
+  }
   return 0;
 }
 
@@ -1718,6 +1810,7 @@ int ewh_lnl_batch(ewh_handle* H, const double* theta_host, int32_t B, double* ou
   int rc;
   if ((rc = ensure_pinned(&H->h_theta, &H->h_theta_cap, (size_t)B * std::max(1, np)))) return rc;
   if (np > 0) std::memcpy(H->h_theta, theta_host, sizeof(double) * (size_t)B * np);
+  if (nd == 1) return lnl_batch_single(H, H->ctx[0], B, out_host);
   std::vector<std::pair<long long, long long>> split;
   if (nd == 1 || H->corr) {
     // samples: contiguous slices (correlated: the cross-pulsar factorisation

@@ -120,3 +120,19 @@ def test_set_fixed_white_in_place(require_gpu):
     fresh.set_default_params(new)
     np.testing.assert_array_equal(fresh.get_lnlikelihood_batch(X), got)
     check_parity(got[8:], oracle_lnl(pta, X[8:]), "c3_small new white noise")
+
+
+def test_graph_replay_matches_eager(require_gpu):
+    """ewh_lnl_batch captures each single-device batch size into a HIP graph
+    on its first call and replays it afterwards; buffer growth (a larger B)
+    invalidates the graphs.  Every call must equal the first (eager) one."""
+    from conftest import load_golden
+    pta, X, _, _ = load_golden("c3_small")
+    big = np.vstack([X] * 32)
+    ref = {1: pta.get_lnlikelihood_batch(X[:1]), 16: pta.get_lnlikelihood_batch(X)}
+    ref[512] = pta.get_lnlikelihood_batch(big)
+    for B in (1, 1, 16, 1, 16, 512, 1, 16, 512, 1):
+        XX = {1: X[:1], 16: X, 512: big}[B]
+        np.testing.assert_array_equal(pta.get_lnlikelihood_batch(XX), ref[B])
+    for i in range(16):                                   # single-theta calls (PTMCMC / bilby)
+        assert pta.get_lnlikelihood(X[i]) == ref[16][i]
