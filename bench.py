@@ -164,6 +164,10 @@ def main():
     ap.add_argument("--kernel-mode", type=int, default=0, help="0 auto (MFMA), 1 LDS fallback")
     ap.add_argument("--config", default="c3", choices=["c3", "c5"],
                     help="c3: the headline 45-pulsar CURN batch (default); c5: 100-pulsar HD-correlated PTA")
+    ap.add_argument("--partition", default="samples", choices=["samples", "pulsars"],
+                    help="c5 only: shard samples (no exchange) or pulsars (all-gather of the kept common blocks, "
+                         "then the dense factorisation on every rank: one proposal over N GPUs)")
+    ap.add_argument("--c5-batch", type=int, default=None, help="c5 proposals per step (default 512 / 1 for pulsars)")
     args = ap.parse_args()
     if args.config == "c5":
         return main_c5(args)
@@ -297,7 +301,9 @@ def main_c5(args):
     dev = torch.device("cuda", local if world > 1 else 0)
     cfg = synth.config_c5()
     pta = cfg.pta
-    Bg = cfg.B
+    if args.partition == "pulsars":
+        return c5_pulsar_partition(args, cfg, world, rank, dev)
+    Bg = args.c5_batch or cfg.B
     X = synth.prior_draws(pta, Bg * world, cfg.theta_seed)[rank * Bg:(rank + 1) * Bg]
     theta = torch.from_numpy(np.ascontiguousarray(X)).to(dev)
     eng = pta.engine(device=dev.index)
@@ -344,6 +350,70 @@ def main_c5(args):
                "roofline": {"bound": "mfma", "achieved": achieved, "peak": FP64_MFMA_PEAK_TFLOPS, "unit": "TFLOP/s",
                             "frac": achieved / FP64_MFMA_PEAK_TFLOPS, "traffic": None,
                             "kernel": "whole step (partial chol + M_g^-1 + dense factorisation)"}}
+        print(json.dumps(rec), flush=True)
+    if world > 1:
+        dist.destroy_process_group()
+
+
+def c5_pulsar_partition(args, cfg, world, rank, dev):
+    """Config 5, the exchange step of SURVEY.md §8(e): rank r runs the partial
+    factorisations of pulsars [r per, (r+1) per) (ewh_corr_partial_device,
+    pulsar-major buffers), one RCCL all-gather moves the kept common blocks
+    and local terms, every rank assembles and factors Sigma_c
+    (ewh_corr_finish_device).  B proposals per step (default 1: a PTMCMC
+    proposal spread over the node)."""
+    import torch
+    import torch.distributed as dist
+    from enterprise_warp_amd import synth
+    pta = cfg.pta
+    B = args.c5_batch or 1
+    X = synth.prior_draws(pta, B, cfg.theta_seed)
+    theta = torch.from_numpy(X).to(dev)
+    eng = pta.engine(device=dev.index)
+    kd = eng.keep_dim()
+    P = len(pta.signal_collections)
+    per = -(-P // world)
+    p0, p1 = min(P, rank * per), min(P, (rank + 1) * per)
+    keep = torch.zeros((world * per, B, kd, kd), dtype=torch.float64, device=dev)
+    local = torch.zeros((world * per, B), dtype=torch.float64, device=dev)
+    out = torch.zeros(B, dtype=torch.float64, device=dev)
+    stream = torch.cuda.current_stream(dev)
+
+    def step():
+        eng.corr_partial_device(theta.data_ptr(), B, p0, p1, keep.data_ptr(), local.data_ptr(), stream.cuda_stream)
+        if world > 1:
+            dist.all_gather_into_tensor(keep, keep[rank * per:(rank + 1) * per].clone())
+            dist.all_gather_into_tensor(local, local[rank * per:(rank + 1) * per].clone())
+        eng.corr_finish_device(theta.data_ptr(), B, keep.data_ptr(), local.data_ptr(), out.data_ptr(),
+                               stream.cuda_stream)
+
+    for _ in range(args.warmup):
+        step()
+    torch.cuda.synchronize(dev)
+    if world > 1:
+        dist.barrier()
+    t0 = time.perf_counter()
+    for _ in range(args.steps):
+        step()
+    torch.cuda.synchronize(dev)
+    if world > 1:
+        dist.barrier()
+    elapsed = time.perf_counter() - t0
+    t = torch.tensor([elapsed], dtype=torch.float64, device=dev)
+    if world > 1:
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+    elapsed = float(t.item())
+    lnl = out.cpu().numpy()
+    if rank == 0:
+        rec = {"metric": "lnL evals/sec, 100-psr HD-correlated PTA, pulsar-partitioned (BASELINE config 5)",
+               "value": B * args.steps / elapsed, "unit": "lnL evals/s", "n_gpus": world, "steps": args.steps,
+               "warmup": args.warmup, "ms_per_step": 1e3 * elapsed / args.steps, "higher_is_better": True,
+               "scaling": "strong", "vs_baseline": None, "dtype": "f64",
+               "data": "synthetic: seeded 100-pulsar x 20k-TOA PTA, HD GWB 14 freqs (SURVEY.md §8(d) C5)",
+               "config": {"workload": "C5, pulsars sharded, kept blocks all-gathered over RCCL",
+                          "global_batch": B, "n_pulsars": P, "parallelism": f"pulsars{world}",
+                          "gather_bytes_per_step": int(world * per * B * (kd * kd + 1) * 8),
+                          "finite_fraction": float(np.mean(np.isfinite(lnl)))}}
         print(json.dumps(rec), flush=True)
     if world > 1:
         dist.destroy_process_group()

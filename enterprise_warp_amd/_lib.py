@@ -52,6 +52,7 @@ class PtaDesc(C.Structure):
 
 
 EXPORTS = ["ewh_create", "ewh_num_devices", "ewh_set_fixed_white", "ewh_lnl_batch", "ewh_lnl_units_device",
+           "ewh_keep_dim", "ewh_corr_partial_device", "ewh_corr_finish_device",
            "ewh_last_unit_terms", "ewh_unit_cost", "ewh_set_kernel_mode", "ewh_optstat", "ewh_destroy",
            "ewh_last_error", "ewh_version"]
 DEV_EXPORTS = ["ewh_dev_gram", "ewh_dev_reduced"]
@@ -91,6 +92,14 @@ def load():
     lib.ewh_lnl_units_device.argtypes = [C.c_void_p, C.c_void_p, C.c_int32, C.c_int64, C.c_int64, C.c_void_p,
                                          C.c_void_p]
     lib.ewh_lnl_units_device.restype = C.c_int
+    lib.ewh_keep_dim.argtypes = [C.c_void_p]
+    lib.ewh_keep_dim.restype = C.c_int
+    lib.ewh_corr_partial_device.argtypes = [C.c_void_p, C.c_void_p, C.c_int32, C.c_int32, C.c_int32, C.c_void_p,
+                                            C.c_void_p, C.c_void_p]
+    lib.ewh_corr_partial_device.restype = C.c_int
+    lib.ewh_corr_finish_device.argtypes = [C.c_void_p, C.c_void_p, C.c_int32, C.c_void_p, C.c_void_p, C.c_void_p,
+                                           C.c_void_p]
+    lib.ewh_corr_finish_device.restype = C.c_int
     lib.ewh_last_unit_terms.argtypes = [C.c_void_p, _dp, C.c_int32]
     lib.ewh_last_unit_terms.restype = C.c_int
     lib.ewh_unit_cost.argtypes = [C.c_void_p, C.c_int32]

@@ -37,6 +37,7 @@ int launch_chol_small(int mode, int nb, const CholJob* jobs, int B, long long u0
       case 11: launch_chol_mfma<8, 1, 2, 6>(jobs, B, u0, n, b_off, theta, ldth, units, st); return 0;  // + row scales by rsqrt_fast (spills)
       case 12: launch_chol_mfma<8, 1, 2, 7>(jobs, B, u0, n, b_off, theta, ldth, units, st); return 0;  // default without the packed row scales
       case 13: launch_chol_mfma<8, 1, 2, 9>(jobs, B, u0, n, b_off, theta, ldth, units, st); return 0;  // phase split H = 3, every row scale packed
+      case 14: launch_chol_mfma<8, 1, 2, 10>(jobs, B, u0, n, b_off, theta, ldth, units, st); return 0;  // ALG 8 + lookahead (trailing MFMAs inside the next panel)
       default: break;
     }
   }

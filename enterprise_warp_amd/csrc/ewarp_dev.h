@@ -587,9 +587,52 @@ __device__ __forceinline__ double row_newbcast_rows(double x) {
   return __builtin_bit_cast(double, v);
 }
 
-template <int NB, int FULL, int ALG, typename BBt, typename Blk>
+// upper-triangle blocks (i, j), r0 <= i < r1, i <= j < NB, enumerated row by
+// row: count, and block t -> (i, j)
+constexpr int tri_count(int nb, int r0, int r1) {
+  int n = 0;
+  for (int i = r0; i < r1; ++i) n += nb - i;
+  return n;
+}
+constexpr int tri_row(int nb, int r0, int t) {
+  int i = r0;
+  while (t >= nb - i) { t -= nb - i; ++i; }
+  return i;
+}
+constexpr int tri_col(int nb, int r0, int t) {
+  int i = r0;
+  while (t >= nb - i) { t -= nb - i; ++i; }
+  return i + t;
+}
+
+struct NoFill {
+  template <typename K>
+  __device__ __forceinline__ void operator()(K) const {}
+  // the blocked panel's E = L^-T of the diagonal block (before V = E^T A) and
+  // each register's row scale D^-1/2: used by the dense diagonal-block kernel
+  __device__ __forceinline__ void on_e(const v4d&) const {}
+  __device__ __forceinline__ void on_scale(int, double) const {}
+};
+
+// a plain per-pivot filler (lambda) with the no-op hooks
+template <typename F>
+struct FillOnly : NoFill {
+  F& f;
+  __device__ __forceinline__ explicit FillOnly(F& g) : f(g) {}
+  template <typename K>
+  __device__ __forceinline__ void operator()(K k) const { f(k); }
+};
+
+// fill(integral_constant<k>) runs after pivot k of the diagonal block (ALG >=
+// 5): the lookahead kernel (ALG 10) hands it the independent trailing updates
+// of the previous block row, so their MFMAs issue inside this panel's
+// latency-bound pivot chain instead of after it.
+// RL: the last column of block row NB-1 is the residual (not pivoted), as in
+// the per-pulsar factorisations; false for a plain SPD block (the dense
+// cross-pulsar factorisation's diagonal blocks).
+template <int NB, int FULL, int ALG, bool RL = true, typename BBt, typename Blk, typename Fill = NoFill>
 __device__ __forceinline__ void panel_ldl_row(BBt BBc, Blk&& blk, int q, int c, LogAcc& ldet, bool& ok,
-                                              double* rowbuf) {
+                                              double* rowbuf, Fill&& fill = Fill{}) {
   constexpr int LD = 16 * NB;
   (void)rowbuf;
   (void)LD;
@@ -611,7 +654,7 @@ __device__ __forceinline__ void panel_ldl_row(BBt BBc, Blk&& blk, int q, int c, 
     });
     static_for<0, 4>([&](auto KR) {
       constexpr int kr = decltype(KR)::value;
-      constexpr int nk = (bb == NB - 1 && kr == 3) ? 3 : 4;   // the r column is not pivoted
+      constexpr int nk = (RL && bb == NB - 1 && kr == 3) ? 3 : 4;   // the r column is not pivoted
       static_for<0, nk>([&](auto KQc) {
         constexpr int kq = decltype(KQc)::value;
         constexpr int k = 4 * kr + kq;
@@ -634,15 +677,17 @@ __device__ __forceinline__ void panel_ldl_row(BBt BBc, Blk&& blk, int q, int c, 
           constexpr int r = decltype(R)::value;
           blk(BBc)[r] = fma(-ui[r], w, blk(BBc)[r]);
         });
-        if constexpr (bb < NB - 1 && k < 15) {
+        if constexpr ((bb < NB - 1 || !RL) && k < 15) {
           const double uc = (c > k) ? w : 0.0;
           static_for<0, kr + 1>([&](auto R) {
             constexpr int r = decltype(R)::value;
             E[r] = fma(-uc, row_newbcast<k>(E[r]), E[r]);
           });
         }
+        fill(std::integral_constant<int, k>{});
       });
     });
+    if constexpr (bb < NB - 1 || !RL) fill.on_e(E);
     static_for<bb + 1, NB>([&](auto JJ) {
       v4d acc = {0.0, 0.0, 0.0, 0.0};
       static_for<0, 4>([&](auto S) {
@@ -764,7 +809,7 @@ __device__ __forceinline__ void panel_ldl_row(BBt BBc, Blk&& blk, int q, int c, 
   // rows of the block row -> U = d^-1/2 V, d of row q + 4r read from the
   // diagonal (lane 17q + 4r); log-det and positivity from one lane per row
   // (c == 0); the r row (last block, row 15) is left as it is
-  if constexpr ((ALG == 8 && bb >= Split<NB, ALG>::H) || ALG == 9) {
+  if constexpr (((ALG == 8 || ALG == 10) && bb >= Split<NB, ALG>::H) || ALG == 9) {
     // (phase 3 only: in phase 1 the extra temporaries spill)
     // packed: lane (q, c) takes d of row q + 4 (c/4) -- held in register c/4
     // of lane (q, q + 4 (c/4)), whose own c/4 is the same -- so one gather,
@@ -773,7 +818,7 @@ __device__ __forceinline__ void panel_ldl_row(BBt BBc, Blk&& blk, int q, int c, 
     const int cr = c >> 2;
     const double own = cr == 0 ? blk(BBc)[0] : cr == 1 ? blk(BBc)[1] : cr == 2 ? blk(BBc)[2] : blk(BBc)[3];
     double dv = __shfl(own, 17 * q + 4 * cr);
-    if constexpr (bb == NB - 1) dv = (q == 3 && cr == 3) ? 1.0 : dv;
+    if constexpr (RL && bb == NB - 1) dv = (q == 3 && cr == 3) ? 1.0 : dv;
     ok = ok && (dv > 0.0);
     if ((c & 3) == 0) ldet.add(dv);
     const double rsp = rsqrt_nr(dv);
@@ -785,12 +830,13 @@ __device__ __forceinline__ void panel_ldl_row(BBt BBc, Blk&& blk, int q, int c, 
   } else
   static_for<0, 4>([&](auto R) {
     constexpr int r = decltype(R)::value;
-    const bool rrow = (bb == NB - 1 && r == 3) && q == 3;
+    const bool rrow = RL && (bb == NB - 1 && r == 3) && q == 3;
     const double dg = __shfl(blk(BBc)[r], 17 * q + 4 * r);
     const double dv = rrow ? 1.0 : dg;
     ok = ok && (dv > 0.0);
     if (c == 0) ldet.add(dv);
     const double rs = rrow ? 1.0 : (ALG == 6 ? rsqrt_fast(dv) : rsqrt_nr(dv));
+    fill.on_scale(r, rs);
     static_for<bb, NB>([&](auto JJ) { blk(JJ)[r] *= rs; });
   });
 }
@@ -798,13 +844,15 @@ __device__ __forceinline__ void panel_ldl_row(BBt BBc, Blk&& blk, int q, int c, 
 // KEEP > 0 (correlated common process): only block rows 0..NB-KEEP-1 (the
 // pulsar's own columns) are factored; the trailing KEEP x KEEP blocks (the
 // common columns + r: their Schur complement S^G, d', rho) are written to
-// keep_out[((b - keep_b0) * keep_P + p)] as a dense (16 KEEP)^2 square, and
+// keep_out[(p * keep_bs + (b - keep_b0))] as a dense (16 KEEP)^2 square
+// (pulsar-major: a device's pulsar range is one contiguous slice, the unit an
+// all-gather moves), and
 // the unit term is the local part K - 1/2 log|Sigma_LL| - 1/2 log|phi_L|.
 template <int NB, int FULL, int W, int ALG = 0, int KEEP = 0>
 __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(W, W)))
 void chol_mfma_kernel(const CholJob* __restrict__ jobs, int B, long long u0, int b_off,
                       const double* __restrict__ theta, int ldth, double* __restrict__ out_units,
-                      double* __restrict__ keep_out, int keep_b0, int keep_P) {
+                      double* __restrict__ keep_out, int keep_b0, int keep_bs) {
   constexpr int LD = 16 * NB;
   using S = Split<NB, ALG>;
   constexpr int H = S::H;
@@ -856,13 +904,13 @@ void chol_mfma_kernel(const CholJob* __restrict__ jobs, int B, long long u0, int
   if constexpr (ALG >= 1) ldet = lphi;
   bool ok = true;
   // LDL^T panel row bb (ALG >= 1)
-  auto panel_ldl = [&](auto BBc, auto&& blk) {
-    panel_ldl_row<NB, FULL, ALG>(BBc, blk, q, c, ldet, ok, rowbuf);
+  auto panel_ldl = [&](auto BBc, auto&& blk, auto&& fill) {
+    panel_ldl_row<NB, FULL, ALG>(BBc, blk, q, c, ldet, ok, rowbuf, FillOnly<std::remove_reference_t<decltype(fill)>>(fill));
   };
   // panel row bb over the blocks blk(j), j = bb..NB-1
-  auto panel = [&](auto BBc, auto&& blk) {
+  auto panel = [&](auto BBc, auto&& blk, auto&& fill) {
     if constexpr (ALG >= 1) {
-      panel_ldl(BBc, blk);
+      panel_ldl(BBc, blk, fill);
       return;
     }
     constexpr int bb = decltype(BBc)::value;
@@ -915,10 +963,26 @@ void chol_mfma_kernel(const CholJob* __restrict__ jobs, int B, long long u0, int
     constexpr int bi = decltype(BI)::value;
     static_for<bi, NB>([&](auto BJ) { load_block(BI, BJ, U1[S::i1(bi, decltype(BJ)::value)]); });
   });
+  // ALG 10 (lookahead): step bb updates only the next row (bb + 1) at once; its
+  // updates of rows >= bb + 2 are spread over the pivots of panel bb + 1
+  // (same blocks, same order per block: bit-identical to ALG 8)
+  constexpr bool LA = ALG == 10;
   static_for<0, H>([&](auto BBc) {
     constexpr int bb = decltype(BBc)::value;
-    panel(BBc, [&](auto JJ) -> v4d& { return U1[S::i1(bb, decltype(JJ)::value)]; });
-    static_for<bb + 1, H>([&](auto II) {
+    auto fill = [&](auto Kc) {
+      if constexpr (LA && bb >= 1) {
+        constexpr int k = decltype(Kc)::value;
+        constexpr int r0 = bb + 1, F = tri_count(NB, r0, H);
+        constexpr int np = (bb == NB - 1) ? 15 : 16;
+        constexpr int t0 = (k * F + np - 1) / np, t1 = ((k + 1) * F + np - 1) / np;
+        static_for<t0, t1>([&](auto T) {
+          constexpr int i = tri_row(NB, r0, decltype(T)::value), j = tri_col(NB, r0, decltype(T)::value);
+          syrk_update(U1[S::i1(i, j)], U1[S::i1(bb - 1, i)], U1[S::i1(bb - 1, j)]);
+        });
+      }
+    };
+    panel(BBc, [&](auto JJ) -> v4d& { return U1[S::i1(bb, decltype(JJ)::value)]; }, fill);
+    static_for<bb + 1, (LA ? (bb + 2 < H ? bb + 2 : H) : H)>([&](auto II) {
       constexpr int i = decltype(II)::value;
       static_for<i, NB>([&](auto JJ) {
         constexpr int j = decltype(JJ)::value;
@@ -943,8 +1007,21 @@ void chol_mfma_kernel(const CholJob* __restrict__ jobs, int B, long long u0, int
   // ---- phase 3: factor A22 (up to the kept blocks) ----
   static_for<H, NB - KEEP>([&](auto BBc) {
     constexpr int bb = decltype(BBc)::value;
-    panel(BBc, [&](auto JJ) -> v4d& { return U2[S::i2(bb, decltype(JJ)::value)]; });
-    static_for<bb + 1, NB>([&](auto II) {
+    auto fill = [&](auto Kc) {
+      if constexpr (LA && bb >= H + 1) {
+        constexpr int k = decltype(Kc)::value;
+        constexpr int r0 = bb + 1, F = tri_count(NB, r0, NB);
+        constexpr int np = (bb == NB - 1) ? 15 : 16;
+        constexpr int t0 = (k * F + np - 1) / np, t1 = ((k + 1) * F + np - 1) / np;
+        static_for<t0, t1>([&](auto T) {
+          constexpr int i = tri_row(NB, r0, decltype(T)::value), j = tri_col(NB, r0, decltype(T)::value);
+          syrk_update(U2[S::i2(i, j)], U2[S::i2(bb - 1, i)], U2[S::i2(bb - 1, j)]);
+        });
+      }
+    };
+    panel(BBc, [&](auto JJ) -> v4d& { return U2[S::i2(bb, decltype(JJ)::value)]; }, fill);
+    constexpr bool last = bb == NB - KEEP - 1;
+    static_for<bb + 1, ((LA && !last) ? (bb + 2 < NB ? bb + 2 : NB) : NB)>([&](auto II) {
       constexpr int i = decltype(II)::value;
       static_for<i, NB>([&](auto JJ) {
         constexpr int j = decltype(JJ)::value;
@@ -957,7 +1034,7 @@ void chol_mfma_kernel(const CholJob* __restrict__ jobs, int B, long long u0, int
     qv = readlane_d(U2[S::i2(NB - 1, NB - 1)][3], 63);
   } else {
     constexpr int KD = 16 * KEEP;
-    double* ko = keep_out + ((long long)(b - keep_b0) * keep_P + p) * (KD * KD);
+    double* ko = keep_out + ((long long)p * keep_bs + (b - keep_b0)) * (KD * KD);
     static_for<NB - KEEP, NB>([&](auto II) {
       constexpr int i = decltype(II)::value;
       static_for<i, NB>([&](auto JJ) {
@@ -1119,8 +1196,9 @@ int launch_chol_small(int mode, int nb, const CholJob* jobs, int B, long long u0
                       const double* theta, int ldth, double* units, hipStream_t st);
 int launch_chol_big_nb(int nb, const CholJob* jobs, int B, long long u0, long long n, int b_off,
                        const double* theta, int ldth, double* units, double* scr, long long cap, hipStream_t st);
+// keep_out: pulsar-major kept blocks, keep_bs samples per pulsar (see chol_mfma_kernel KEEP)
 int launch_partial_nb(int nb, int keep, const CholJob* jobs, int B, long long u0, long long n,
-                      const double* theta, int ldth, double* units, double* keep_out, int P, hipStream_t st);
+                      const double* theta, int ldth, double* units, double* keep_out, int keep_bs, hipStream_t st);
 // dynamic-LDS attributes of the contraction kernels on the current device
 int set_contract_attributes();
 // true in the dev library (make dev, -DEWH_DEV): kernel A/B modes 3-6, 8-13 compiled in

@@ -383,18 +383,22 @@ __global__ __launch_bounds__(256) void common_minv_reg_kernel(const CommonPsr* _
 
 // Dense Sigma_c (Np x Np, row-major) of sample bl, one row per workgroup:
 // rows/cols (a, g) -> a nc + g; r at Np - 1; pad rows/cols identity.
+// keep: pulsar-major kept blocks, Bk samples per pulsar; this chunk starts at
+// sample b0 (pulsar a's block of sample bl at keep[(a Bk + b0 + bl) KD^2]).
 __global__ __launch_bounds__(256) void common_assemble_kernel(const double* __restrict__ keep, int KD, int P, int nc,
+                                                              long long Bk, int b0,
                                                               const double* __restrict__ minv,
                                                               const int* __restrict__ rep, int Np,
                                                               double* __restrict__ mats) {
   const int i = blockIdx.x, bl = blockIdx.y;
   const int N = P * nc;
+  const long long ps = Bk * KD * KD;                                // pulsar stride
   double* row = mats + ((long long)bl * Np + i) * Np;
-  const double* kb = keep + (long long)bl * P * KD * KD;
+  const double* kb = keep + (long long)(b0 + bl) * KD * KD;
   const double* mb = minv + (long long)bl * nc * P * P;
   if (i < N) {
     const int a = i / nc, g = i - a * nc;
-    const double* ka = kb + (long long)a * KD * KD + g * KD;       // row g of pulsar a's kept square
+    const double* ka = kb + (long long)a * ps + g * KD;            // row g of pulsar a's kept square
     const double* mg = mb + (long long)rep[g] * P * P + (long long)a * P;  // row a of M_g^-1
     for (int j = threadIdx.x; j < Np; j += 256) {
       double v = 0.0;
@@ -412,9 +416,9 @@ __global__ __launch_bounds__(256) void common_assemble_kernel(const double* __re
       double v = 0.0;
       if (j < N) {
         const int bb = j / nc, h = j - bb * nc;
-        v = kb[(long long)bb * KD * KD + (KD - 1) * KD + h];
+        v = kb[(long long)bb * ps + (KD - 1) * KD + h];
       } else if (j == Np - 1) {
-        for (int a = 0; a < P; ++a) v += kb[(long long)a * KD * KD + KD * KD - 1];
+        for (int a = 0; a < P; ++a) v += kb[(long long)a * ps + KD * KD - 1];
       }
       row[j] = v;
     }
@@ -483,6 +487,128 @@ __global__ __launch_bounds__(256) void dchol_diag_kernel(double* __restrict__ ma
     if (!ok) fail[bl] = 1;
     if (last) qout[bl] = qlast;
   }
+}
+
+// ---- register-resident diagonal block + panel (the default) -------------
+// wbuf per sample (DW doubles): slots of 256 doubles in the MFMA C/D lane
+// layout (lane l holds 4 consecutive doubles: register r <-> row (l>>4) + 4r,
+// column l&15) -- E_s = L_ss^-T of the 16-row sub-blocks s = 0..3 (slots
+// 0-3), their row scales D_s^-1/2 (4-7), the scaled factor blocks U_st,
+// s < t (8-13: 01 02 03 12 13 23).
+constexpr int DW_SLOTS = 14;
+__host__ __device__ constexpr int dw_u(int s, int t) { return 8 + (s == 0 ? t - 1 : s == 1 ? t + 1 : 5); }
+
+struct DiagHook : NoFill {
+  double* W;
+  int bb;
+  __device__ __forceinline__ void on_e(const v4d& E) const { *(v4d*)(W + bb * 256) = E; }
+  __device__ __forceinline__ void on_scale(int r, double rs) const { W[(4 + bb) * 256 + r] = rs; }
+};
+
+// One wave per sample: the 64 x 64 diagonal block k of Sigma_c factored in
+// registers by the blocked LDL^T panel of chol_mfma_kernel (NB = 4, no
+// residual column except in the LAST block, whose last pivot is
+// q_c = rho - d'^T Sigma_c^-1 d'); log-det and positivity accumulated; E_s,
+// D_s^-1/2 and U_st written for dchol_panel_reg_kernel.
+template <bool LAST>
+__global__ __launch_bounds__(64) void dchol_diag_reg_kernel(double* __restrict__ mats, int Np, int k,
+                                                            double* __restrict__ wbuf, double* __restrict__ ldet,
+                                                            double* __restrict__ qout, int* __restrict__ fail) {
+  const int bl = blockIdx.x, lane = threadIdx.x, q = lane >> 4, c = lane & 15;
+  const double* A = mats + (long long)bl * Np * Np + (long long)(DCB * k) * Np + DCB * k;
+  double* W = wbuf + (long long)bl * DW_SLOTS * 256 + lane * 4;
+  constexpr auto id = [](int i, int j) { return i * 4 - i * (i - 1) / 2 + (j - i); };
+  v4d U[10];
+  static_for<0, 4>([&](auto I) {
+    constexpr int i = decltype(I)::value;
+    static_for<i, 4>([&](auto J) {
+      constexpr int j = decltype(J)::value;
+      static_for<0, 4>([&](auto R) {
+        constexpr int r = decltype(R)::value;
+        U[id(i, j)][r] = A[(long long)(16 * i + q + 4 * r) * Np + 16 * j + c];
+      });
+    });
+  });
+  LogAcc ld;
+  bool ok = true;
+  static_for<0, 4>([&](auto BBc) {
+    constexpr int bb = decltype(BBc)::value;
+    DiagHook hk;
+    hk.W = W;
+    hk.bb = bb;
+    panel_ldl_row<4, 1, 7, LAST>(BBc, [&](auto JJ) -> v4d& { return U[id(bb, decltype(JJ)::value)]; }, q, c, ld, ok,
+                                 nullptr, hk);
+    static_for<bb + 1, 4>([&](auto II) {
+      constexpr int i = decltype(II)::value;
+      static_for<i, 4>([&](auto JJ) {
+        constexpr int j = decltype(JJ)::value;
+        syrk_update(U[id(i, j)], U[id(bb, i)], U[id(bb, j)]);
+      });
+    });
+  });
+  if constexpr (!LAST) {
+    static_for<0, 4>([&](auto SS) {
+      constexpr int s0 = decltype(SS)::value;
+      static_for<s0 + 1, 4>([&](auto TT) {
+        constexpr int t0 = decltype(TT)::value;
+        *(v4d*)(W + dw_u(s0, t0) * 256) = U[id(s0, t0)];
+      });
+    });
+  }
+  const double ldv = wave_sum(ld.value());
+  const bool ok_all = __all(ok);
+  double qv = 0.0;
+  if constexpr (LAST) qv = readlane_d(U[id(3, 3)][3], 63);
+  if (lane == 0) {
+    ldet[bl] += ldv;
+    if (!ok_all) fail[bl] = 1;
+    if (LAST) qout[bl] = qv;
+  }
+}
+
+// U_kj = L_kk^-1 A_kj (scaled) for the tiles j > k: one wave per (16-column
+// strip, tile, sample), the strip's four 16 x 16 blocks in registers, the
+// block forward substitution by fp64 MFMA with the operands of wbuf.
+__global__ __launch_bounds__(64) void dchol_panel_reg_kernel(double* __restrict__ mats, int Np, int k,
+                                                             const double* __restrict__ wbuf) {
+  const int strip = blockIdx.x & 3, jt = blockIdx.x >> 2, bl = blockIdx.y;
+  const int lane = threadIdx.x, q = lane >> 4, c = lane & 15;
+  const int j = k + 1 + jt;
+  double* T = mats + (long long)bl * Np * Np + (long long)(DCB * k) * Np + DCB * j + 16 * strip;
+  const double* W = wbuf + (long long)bl * DW_SLOTS * 256 + lane * 4;
+  v4d a[4];
+  static_for<0, 4>([&](auto SS) {
+    constexpr int s0 = decltype(SS)::value;
+    static_for<0, 4>([&](auto R) {
+      constexpr int r = decltype(R)::value;
+      a[s0][r] = T[(long long)(16 * s0 + q + 4 * r) * Np + c];
+    });
+  });
+  static_for<0, 4>([&](auto SS) {
+    constexpr int s0 = decltype(SS)::value;
+    static_for<0, s0>([&](auto TT) {
+      constexpr int t0 = decltype(TT)::value;
+      syrk_update(a[s0], *(const v4d*)(W + dw_u(t0, s0) * 256), a[t0]);
+    });
+    const v4d E = *(const v4d*)(W + s0 * 256);
+    const v4d rs = *(const v4d*)(W + (4 + s0) * 256);
+    v4d acc = {0.0, 0.0, 0.0, 0.0};
+    static_for<0, 4>([&](auto S2) {
+      constexpr int sk = decltype(S2)::value;
+      acc = __builtin_amdgcn_mfma_f64_16x16x4f64(E[sk], a[s0][sk], acc, 0, 0, 0);
+    });
+    static_for<0, 4>([&](auto R) {
+      constexpr int r = decltype(R)::value;
+      a[s0][r] = acc[r] * rs[r];
+    });
+  });
+  static_for<0, 4>([&](auto SS) {
+    constexpr int s0 = decltype(SS)::value;
+    static_for<0, 4>([&](auto R) {
+      constexpr int r = decltype(R)::value;
+      T[(long long)(16 * s0 + q + 4 * r) * Np + c] = a[s0][r];
+    });
+  });
 }
 
 // stage a 64 x 64 tile (row stride ld) into LDS [64][64 + 1]
@@ -619,7 +745,7 @@ __global__ __launch_bounds__(64) void os_xz_kernel(const double* __restrict__ ke
   __shared__ double M[32][33];
   __shared__ double colk[32], rowk[32], dv[32], kr[32], sq[32];
   const int a = blockIdx.x, bl = blockIdx.y, t = threadIdx.x;
-  const double* K = keep + ((long long)bl * P + a) * KD * KD;
+  const double* K = keep + ((long long)a * gridDim.y + bl) * KD * KD;     // pulsar-major, B = gridDim.y
   const double* th = theta + (long long)bl * ldth;
   for (int idx = t; idx < nc * nc; idx += 64) M[idx / nc][idx % nc] = K[(idx / nc) * KD + idx % nc];
   if (t < nc) {
@@ -1233,13 +1359,10 @@ int ensure_common_scratch(DevCtx* h, int B) {
   return 0;
 }
 
-// correlated batch: per-pulsar partial factorisations of every unit, then per
-// sample chunk the common-block assembly and the dense factorisation
-int lnl_correlated(DevCtx* h, const double* theta_dev, int B, hipStream_t st) {
-  const int P = h->P, ldth = h->n_param, KD = 16 * h->keep;
+int ensure_keep(DevCtx* h, int B) {
+  const int KD = 16 * h->keep;
   int rc;
-  if ((rc = ensure_common_scratch(h, B))) return rc;
-  const size_t need = (size_t)B * P * KD * KD;
+  const size_t need = (size_t)B * h->P * KD * KD;
   if (need > h->keep_cap) {
     if (h->d_keep) {
       (void)hipFree(h->d_keep);
@@ -1250,18 +1373,37 @@ int lnl_correlated(DevCtx* h, const double* theta_dev, int B, hipStream_t st) {
     if ((rc = dalloc(h, &h->d_keep, need))) return rc;
     h->keep_cap = need;
   }
-  const long long U = (long long)P * B;
-  for (long long u = 0; u < U;) {
+  return 0;
+}
+
+// Step 1 of a correlated batch for pulsars [p_begin, p_end): the partial
+// factorisations (own columns eliminated), writing each unit's local term to
+// units[p B + b] and its kept common block to keep (pulsar-major, B samples
+// per pulsar).
+int corr_partial(DevCtx* h, const double* theta_dev, int B, int p_begin, int p_end, double* units, double* keep,
+                 hipStream_t st) {
+  int rc;
+  for (long long u = (long long)p_begin * B; u < (long long)p_end * B;) {
     const int p0 = (int)(u / B);
     const int nb0 = h->psr[p0].fx_nb;
     int p1 = p0 + 1;
-    while (p1 < P && h->psr[p1].fx_nb == nb0) ++p1;
+    while (p1 < p_end && h->psr[p1].fx_nb == nb0) ++p1;
     const long long seg_end = (long long)p1 * B;
-    if ((rc = launch_partial_nb(nb0, h->keep, h->d_jobs_fixed, B, u, seg_end - u, theta_dev, ldth, h->d_units,
-                               h->d_keep, P, st)))
+    if ((rc = launch_partial_nb(nb0, h->keep, h->d_jobs_fixed, B, u, seg_end - u, theta_dev, h->n_param, units,
+                                keep, B, st)))
       return rc;
     u = seg_end;
   }
+  return 0;
+}
+
+// Step 2, once every pulsar's kept block is in `keep`: per sample chunk the
+// M_g inverses, the dense Sigma_c assembly and factorisation; the global term
+// of sample b goes to units[P B + b].
+int corr_finish(DevCtx* h, const double* theta_dev, int B, const double* keep, double* units, hipStream_t st) {
+  const int P = h->P, ldth = h->n_param, KD = 16 * h->keep;
+  int rc;
+  if ((rc = ensure_common_scratch(h, B))) return rc;
   const int nbk = h->Np / DCB;
   const size_t lds = ((size_t)P * (P + 1) + 3 * P) * sizeof(double);
   for (int c0 = 0; c0 < B; c0 += h->cchunk) {
@@ -1272,9 +1414,8 @@ int lnl_correlated(DevCtx* h, const double* theta_dev, int B, hipStream_t st) {
     else
       hipLaunchKernelGGL(common_minv_kernel, dim3(h->nuniq, nb), dim3(256), lds, st, h->d_cps, P, h->d_orf,
                          h->d_cspec, h->nc, h->d_cuniq, theta_dev, ldth, c0, h->d_minv, h->d_mlog);
-    hipLaunchKernelGGL(common_assemble_kernel, dim3(h->Np, nb), dim3(256), 0, st,
-                       h->d_keep + (size_t)c0 * P * KD * KD, KD, P, h->nc, h->d_minv, h->d_crep, h->Np,
-                       h->d_dense);
+    hipLaunchKernelGGL(common_assemble_kernel, dim3(h->Np, nb), dim3(256), 0, st, keep, KD, P, h->nc,
+                       (long long)B, c0, h->d_minv, h->d_crep, h->Np, h->d_dense);
     EWH_HIP(hipMemsetAsync(h->d_cldet, 0, sizeof(double) * nb, st));
     EWH_HIP(hipMemsetAsync(h->d_cq, 0, sizeof(double) * nb, st));
     EWH_HIP(hipMemsetAsync(h->d_cfail, 0, sizeof(int) * nb, st));
@@ -1282,19 +1423,38 @@ int lnl_correlated(DevCtx* h, const double* theta_dev, int B, hipStream_t st) {
       const int m = nbk - k - 1;
       if (h->kernel_mode != 7 && k > 0)     // row-oriented update of block row k (default)
         hipLaunchKernelGGL(dchol_rowupdate_kernel, dim3(m + 1, nb), dim3(256), 0, st, h->d_dense, h->Np, k);
-      hipLaunchKernelGGL(dchol_diag_kernel, dim3(nb), dim3(256), 0, st, h->d_dense, h->Np, k, h->d_wbuf, h->d_cldet,
-                         h->d_cq, h->d_cfail);
-      if (m > 0) {
-        hipLaunchKernelGGL(dchol_panel_kernel, dim3(m, nb), dim3(256), 0, st, h->d_dense, h->Np, k, h->d_wbuf);
-        if (h->kernel_mode == 7)            // A/B: right-looking trailing update
-          hipLaunchKernelGGL(dchol_update_kernel, dim3(m * (m + 1) / 2, nb), dim3(256), 0, st, h->d_dense, h->Np, k);
+      if (h->kernel_mode == 7 || h->kernel_mode == 1) {   // A/B: round-1 LDS diagonal block + LDS-staged panel
+        hipLaunchKernelGGL(dchol_diag_kernel, dim3(nb), dim3(256), 0, st, h->d_dense, h->Np, k, h->d_wbuf,
+                           h->d_cldet, h->d_cq, h->d_cfail);
+        if (m > 0)
+          hipLaunchKernelGGL(dchol_panel_kernel, dim3(m, nb), dim3(256), 0, st, h->d_dense, h->Np, k, h->d_wbuf);
+      } else {
+        if (m > 0)
+          hipLaunchKernelGGL(HIP_KERNEL_NAME(dchol_diag_reg_kernel<false>), dim3(nb), dim3(64), 0, st, h->d_dense,
+                             h->Np, k, h->d_wbuf, h->d_cldet, h->d_cq, h->d_cfail);
+        else
+          hipLaunchKernelGGL(HIP_KERNEL_NAME(dchol_diag_reg_kernel<true>), dim3(nb), dim3(64), 0, st, h->d_dense,
+                             h->Np, k, h->d_wbuf, h->d_cldet, h->d_cq, h->d_cfail);
+        if (m > 0)
+          hipLaunchKernelGGL(dchol_panel_reg_kernel, dim3(4 * m, nb), dim3(64), 0, st, h->d_dense, h->Np, k,
+                             h->d_wbuf);
       }
+      if (m > 0 && h->kernel_mode == 7)   // A/B: right-looking trailing update
+        hipLaunchKernelGGL(dchol_update_kernel, dim3(m * (m + 1) / 2, nb), dim3(256), 0, st, h->d_dense, h->Np, k);
     }
     hipLaunchKernelGGL(common_final_kernel, dim3((nb + 255) / 256), dim3(256), 0, st, h->d_cldet, h->d_cq,
-                       h->d_cfail, h->d_mlog, h->d_crep, h->nc, nb, c0, P, B, h->d_units);
+                       h->d_cfail, h->d_mlog, h->d_crep, h->nc, nb, c0, P, B, units);
     EWH_HIP(hipGetLastError());
   }
   return 0;
+}
+
+// correlated batch on one device: step 1 for every pulsar, then step 2
+int lnl_correlated(DevCtx* h, const double* theta_dev, int B, hipStream_t st) {
+  int rc;
+  if ((rc = ensure_keep(h, B)) || (rc = corr_partial(h, theta_dev, B, 0, h->P, h->d_units, h->d_keep, st)))
+    return rc;
+  return corr_finish(h, theta_dev, B, h->d_keep, h->d_units, st);
 }
 
 }  // namespace
@@ -1582,7 +1742,7 @@ int ctx_optstat(DevCtx* h, const double* theta_host, int32_t B, const double* ph
     while (p1 < P && h->psr[p1].fx_nb == nb0) ++p1;
     const long long seg_end = (long long)p1 * B;
     if ((rc = launch_partial_nb(nb0, h->keep, h->d_jobs_fixed, B, u, seg_end - u, th, h->n_param, h->d_units,
-                                h->d_keep, P, st))) {
+                                h->d_keep, B, st))) {
       release();
       return rc;
     }
@@ -1662,6 +1822,61 @@ int enqueue_single(ewh_handle* H, DevCtx* h, int B) {
 }
 
 constexpr size_t GRAPH_CACHE = 8;
+
+// Correlated common process, batch smaller than the device count (one
+// PTMCMC proposal): the pulsars are split over the devices (the exchange step
+// of SURVEY.md §8(e)) -- each device runs the partial factorisations of its
+// pulsars, its kept common blocks and local terms are copied peer-to-peer into
+// the first device's buffers (the all-gather), and the first device assembles
+// and factors Sigma_c.  Per-pulsar results do not depend on the device, so the
+// value equals the one-device result bit for bit.
+int lnl_batch_corr_pulsars(ewh_handle* H, int B, double* out_host) {
+  const int nd = (int)H->ctx.size(), P = H->P, np = H->n_param;
+  DevCtx* h0 = H->ctx[0];
+  const size_t kd2 = (size_t)(16 * h0->keep) * (16 * h0->keep);
+  int rc;
+  if ((rc = ensure_pinned(&H->h_out, &H->h_out_cap, (size_t)B))) return rc;
+  for (int i = 0; i < nd; ++i) {
+    DevCtx* h = H->ctx[i];
+    EWH_HIP(hipSetDevice(h->device));
+    if ((rc = ensure_io(h, B)) || (rc = ensure_units(h, B)) || (rc = ensure_keep(h, B))) return rc;
+  }
+  EWH_HIP(hipSetDevice(h0->device));
+  EWH_HIP(hipMemsetAsync(h0->d_units, 0, sizeof(double) * (size_t)(P + 1) * B, h0->stream));
+  EWH_HIP(hipStreamSynchronize(h0->stream));
+  for (int i = 0; i < nd; ++i) {
+    DevCtx* h = H->ctx[i];
+    const int p0 = (int)((long long)P * i / nd), p1 = (int)((long long)P * (i + 1) / nd);
+    if (p1 <= p0) continue;
+    EWH_HIP(hipSetDevice(h->device));
+    if (np > 0)
+      EWH_HIP(hipMemcpyAsync(h->d_theta, H->h_theta, sizeof(double) * (size_t)B * np, hipMemcpyHostToDevice,
+                             h->stream));
+    if ((rc = corr_partial(h, h->d_theta, B, p0, p1, h->d_units, h->d_keep, h->stream))) return rc;
+    if (i > 0) {   // gather: this device's pulsar slices into the first device
+      EWH_HIP(hipMemcpyPeerAsync(h0->d_keep + (size_t)p0 * B * kd2, h0->device, h->d_keep + (size_t)p0 * B * kd2,
+                                 h->device, sizeof(double) * (size_t)(p1 - p0) * B * kd2, h->stream));
+      EWH_HIP(hipMemcpyPeerAsync(h0->d_units + (size_t)p0 * B, h0->device, h->d_units + (size_t)p0 * B, h->device,
+                                 sizeof(double) * (size_t)(p1 - p0) * B, h->stream));
+    }
+  }
+  for (int i = 1; i < nd; ++i) {
+    EWH_HIP(hipSetDevice(H->ctx[i]->device));
+    EWH_HIP(hipStreamSynchronize(H->ctx[i]->stream));
+  }
+  EWH_HIP(hipSetDevice(h0->device));
+  if ((rc = corr_finish(h0, h0->d_theta, B, h0->d_keep, h0->d_units, h0->stream))) return rc;
+  hipLaunchKernelGGL(reduce_units_kernel, dim3((B + 255) / 256), dim3(256), 0, h0->stream, h0->d_units, P + 1, B,
+                     h0->d_out);
+  EWH_HIP(hipGetLastError());
+  EWH_HIP(hipMemcpyAsync(H->h_out, h0->d_out, sizeof(double) * B, hipMemcpyDeviceToHost, h0->stream));
+  EWH_HIP(hipStreamSynchronize(h0->stream));
+  std::memcpy(out_host, H->h_out, sizeof(double) * B);
+  H->last_split.assign(1, {0, (long long)P * B});     // unit terms live on the first device
+  H->last_B = B;
+  h0->last_B = B;
+  return 0;
+}
 
 // One device: replay the captured graph of this batch size when there is one;
 // otherwise run the batch eagerly (that also sizes every scratch buffer) and
@@ -1774,7 +1989,7 @@ int ewh_set_fixed_white(ewh_handle* H, const double* values) {
 }
 
 int ewh_set_kernel_mode(ewh_handle* H, int32_t mode) {
-  if (!H || mode < 0 || mode > 13) return set_err(EWH_E_INVALID, "bad handle / mode");
+  if (!H || mode < 0 || mode > 14) return set_err(EWH_E_INVALID, "bad handle / mode");
   if (mode >= 3 && mode != 7 && !ab_variants_built())
     return set_err(EWH_E_UNSUPPORTED, "kernel A/B variants are built only into the dev library (make dev)");
   for (DevCtx* h : H->ctx) {
@@ -1811,6 +2026,7 @@ int ewh_lnl_batch(ewh_handle* H, const double* theta_host, int32_t B, double* ou
   if ((rc = ensure_pinned(&H->h_theta, &H->h_theta_cap, (size_t)B * std::max(1, np)))) return rc;
   if (np > 0) std::memcpy(H->h_theta, theta_host, sizeof(double) * (size_t)B * np);
   if (nd == 1) return lnl_batch_single(H, H->ctx[0], B, out_host);
+  if (H->corr && B < nd) return lnl_batch_corr_pulsars(H, B, out_host);
   std::vector<std::pair<long long, long long>> split;
   if (nd == 1 || H->corr) {
     // samples: contiguous slices (correlated: the cross-pulsar factorisation
@@ -1865,6 +2081,43 @@ int ewh_lnl_batch(ewh_handle* H, const double* theta_host, int32_t B, double* ou
   }
   H->last_split = split;
   H->last_B = B;
+  return 0;
+}
+
+int ewh_keep_dim(const ewh_handle* H) {
+  if (!H || !H->corr) return 0;
+  return 16 * H->ctx[0]->keep;
+}
+
+int ewh_corr_partial_device(ewh_handle* H, const double* theta_dev, int32_t B, int32_t p_begin, int32_t p_end,
+                            double* keep_dev, double* local_dev, void* stream) {
+  if (!H || !H->corr || !theta_dev || !keep_dev || !local_dev || B <= 0 || p_begin < 0 || p_end > H->P ||
+      p_begin > p_end)
+    return set_err(EWH_E_INVALID, "bad arguments (needs a correlated-common-process handle)");
+  DevCtx* h = H->ctx[0];
+  EWH_HIP(hipSetDevice(h->device));
+  int rc = corr_partial(h, theta_dev, B, p_begin, p_end, local_dev, keep_dev, (hipStream_t)stream);
+  if (rc) return rc;
+  EWH_HIP(hipGetLastError());
+  return 0;
+}
+
+int ewh_corr_finish_device(ewh_handle* H, const double* theta_dev, int32_t B, const double* keep_dev,
+                           const double* local_dev, double* out_dev, void* stream) {
+  if (!H || !H->corr || !theta_dev || !keep_dev || !local_dev || !out_dev || B <= 0)
+    return set_err(EWH_E_INVALID, "bad arguments (needs a correlated-common-process handle)");
+  DevCtx* h = H->ctx[0];
+  hipStream_t st = (hipStream_t)stream;
+  EWH_HIP(hipSetDevice(h->device));
+  int rc;
+  if ((rc = ensure_units(h, B))) return rc;
+  EWH_HIP(hipMemcpyAsync(h->d_units, local_dev, sizeof(double) * (size_t)H->P * B, hipMemcpyDeviceToDevice, st));
+  if ((rc = corr_finish(h, theta_dev, B, keep_dev, h->d_units, st))) return rc;
+  hipLaunchKernelGGL(reduce_units_kernel, dim3((B + 255) / 256), dim3(256), 0, st, h->d_units, H->P + 1, B, out_dev);
+  EWH_HIP(hipGetLastError());
+  H->last_split.assign(1, {0, (long long)H->P * B});
+  H->last_B = B;
+  h->last_B = B;
   return 0;
 }
 

@@ -439,6 +439,24 @@ class Engine:
         _lib.check(self.lib.ewh_lnl_units_device(self.h, C.c_void_p(theta_ptr), int(B), int(u0), int(u1),
                                                  C.c_void_p(out_ptr), C.c_void_p(stream or 0)))
 
+    def keep_dim(self):
+        """Side of the kept common block of one (pulsar, sample) (0 when the
+        model has no correlated common process)."""
+        return int(self.lib.ewh_keep_dim(self.h))
+
+    def corr_partial_device(self, theta_ptr, B, p0, p1, keep_ptr, local_ptr, stream=None):
+        """Pulsar-partitioned step 1 (ewh_corr_partial_device): pulsars
+        [p0, p1) into the pulsar-major keep [P, B, kd, kd] / local [P, B]."""
+        _lib.check(self.lib.ewh_corr_partial_device(self.h, C.c_void_p(theta_ptr), int(B), int(p0), int(p1),
+                                                    C.c_void_p(keep_ptr), C.c_void_p(local_ptr),
+                                                    C.c_void_p(stream or 0)))
+
+    def corr_finish_device(self, theta_ptr, B, keep_ptr, local_ptr, out_ptr, stream=None):
+        """Pulsar-partitioned step 2 (ewh_corr_finish_device) on the gathered arrays."""
+        _lib.check(self.lib.ewh_corr_finish_device(self.h, C.c_void_p(theta_ptr), int(B), C.c_void_p(keep_ptr),
+                                                   C.c_void_p(local_ptr), C.c_void_p(out_ptr),
+                                                   C.c_void_p(stream or 0)))
+
     def optstat(self, theta, phihat, want_pairs=True):
         """ewh_optstat: (rho [B, P, P], sig [B, P, P], OS [B], OS_sig [B])."""
         theta = np.ascontiguousarray(theta, dtype=float)

@@ -198,6 +198,27 @@ int ewh_lnl_units_device(ewh_handle* h, const double* theta_dev, int32_t B,
                          int64_t unit_begin, int64_t unit_end, double* out_dev,
                          void* stream);
 
+/* Correlated common process, pulsar-partitioned (the exchange step of
+ * one proposal spread over several GPUs, one process per
+ * GPU).  kd = ewh_keep_dim(h) (0 for other handles): the kept common block
+ * of one (pulsar, sample) is kd x kd doubles.
+ *   ewh_corr_partial_device: partial factorisations of pulsars
+ *     [p_begin, p_end) for samples [0, B): local terms to
+ *     local_dev[p * B + b], kept blocks to keep_dev[(p * B + b) * kd * kd]
+ *     (pulsar-major: a rank's pulsar range is one contiguous slice of both
+ *     arrays; other rows are not written).
+ *   -- all-gather keep_dev / local_dev over the ranks (RCCL) --
+ *   ewh_corr_finish_device: with every pulsar's rows present, M_g^-1, the
+ *     dense Sigma_c and its factorisation; out_dev[b] = lnL.
+ * Device pointers on the handle's first device; asynchronous on `stream`.
+ * ewh_lnl_batch uses the same split across the handle's devices (peer
+ * copies instead of RCCL) when B is smaller than the device count. */
+int ewh_keep_dim(const ewh_handle* h);
+int ewh_corr_partial_device(ewh_handle* h, const double* theta_dev, int32_t B, int32_t p_begin, int32_t p_end,
+                            double* keep_dev, double* local_dev, void* stream);
+int ewh_corr_finish_device(ewh_handle* h, const double* theta_dev, int32_t B, const double* keep_dev,
+                           const double* local_dev, double* out_dev, void* stream);
+
 /* Optimal statistic (first device of the handle; the reference's results.py:653-795 ->
  * enterprise_extensions OptimalStatistic.compute_os) for B noise-parameter
  * draws, on a handle created with common->kind == EWH_COMMON_OPTSTAT (fixed

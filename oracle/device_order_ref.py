@@ -355,28 +355,40 @@ class DeviceOrderPTA:
             mins.append(np.linalg.eigvalsh(S * sc[:, None] * sc[None, :])[0])
         return float(min(mins))
 
-    def _lnl_correlated(self, p):
+    def partial(self, i, params):
+        """Step 1 of the correlated likelihood for pulsar i (what
+        ewh_corr_partial_device computes): its local term K_i - 1/2 log|Sigma_LL|
+        - 1/2 log|phi_L| (-inf when the own block is not positive definite) and
+        its kept block, as one (nc + 1)^2 array [[S^G, d'], [d'^T, rho]]."""
         dt = self.dt
+        p = params if all(isinstance(v, (np.ndarray, dt)) for v in params.values()) else _cast(params, dt)
+        pp = self.pulsars[i]
+        S, K, ok, own, com, gstart = self.cache[i] if self.white_fixed else self._reduce(i, p)
+        nc = len(com)
+        phi = phi_columns(pp, p, dt, with_common=False)[own]
+        A = S.copy()
+        idx = np.arange(len(own))
+        A[idx, idx] += 1 / phi
+        d, A = ldl_blocked(A, gstart)
+        local = K - np.sum(np.log(d)) / 2 - np.sum(np.log(phi)) / 2 if ok and np.all(d > 0) else dt(-np.inf)
+        kb = A[gstart:, gstart:]
+        keep = np.zeros((nc + 1, nc + 1), dtype=dt)
+        keep[:nc, :nc] = kb[:nc, :nc]
+        keep[:nc, nc] = kb[:nc, -1]
+        keep[nc, :nc] = kb[-1, :nc]
+        keep[nc, nc] = kb[-1, -1]
+        return local, keep
+
+    def finish(self, params, locals_, keeps):
+        """Step 2 (ewh_corr_finish_device): from every pulsar's local term and
+        kept block, M_g^-1, the dense Sigma_c, its factorisation, lnL."""
+        dt = self.dt
+        p = _cast(params, dt)
         P = len(self.pulsars)
-        keeps, local = [], dt(0)
-        nc = None
-        own_phi_common = []
-        for i, pp in enumerate(self.pulsars):
-            S, K, ok, own, com, gstart = self.cache[i] if self.white_fixed else self._reduce(i, p)
-            nc = len(com)
-            phi_all = phi_columns(pp, p, dt, with_common=False)
-            phi = phi_all[own]
-            own_phi_common.append(phi_all[com])
-            A = S.copy()
-            idx = np.arange(len(own))
-            A[idx, idx] += 1 / phi
-            d, A = ldl_blocked(A, gstart)
-            if not ok or not np.all(d > 0):
-                return -np.inf
-            local += K - np.sum(np.log(d)) / 2 - np.sum(np.log(phi)) / 2
-            kb = A[gstart:, gstart:]
-            keeps.append((kb[:nc, :nc], kb[:nc, -1], kb[-1, -1]))
-        # common spectrum and ORF
+        if not np.all(np.isfinite(np.asarray(locals_, dtype=float))):
+            return dt(-np.inf)
+        nc = keeps[0].shape[0] - 1
+        own_phi_common = [phi_columns(pp, p, dt, with_common=False)[self._common_cols(pp)] for pp in self.pulsars]
         pp0 = self.pulsars[0]
         gc = next(g for g in pp0.gps if g.get("orf"))
         phic = _spectrum(gc, p, dt)
@@ -389,20 +401,24 @@ class DeviceOrderPTA:
             M = Gam * phic[g] + np.diag(np.array([own_phi_common[a][g] for a in range(P)], dtype=dt))
             Minv, ld, ok = _gauss_jordan(M)
             if not ok:
-                return -np.inf
+                return dt(-np.inf)
             mlog += ld
             ix = np.arange(P) * nc + g
             Sc[np.ix_(ix, ix)] += Minv
-        for a, (SG, dG, rho) in enumerate(keeps):
+        for a, kp in enumerate(keeps):
             s = slice(a * nc, (a + 1) * nc)
-            Sc[s, s] += SG
-            Sc[s, N] = dG
-            Sc[N, s] = dG
-            Sc[N, N] += rho
+            Sc[s, s] += kp[:nc, :nc]
+            Sc[s, N] = kp[:nc, nc]
+            Sc[N, s] = kp[nc, :nc]
+            Sc[N, N] += kp[nc, nc]
         d, A = ldl_blocked(Sc, N, bs=64)
         if not np.all(d > 0):
-            return -np.inf
-        return local - (np.sum(np.log(d)) + A[N, N] + mlog) / 2
+            return dt(-np.inf)
+        return sum(locals_) - (np.sum(np.log(d)) + A[N, N] + mlog) / 2
+
+    def _lnl_correlated(self, p):
+        parts = [self.partial(i, p) for i in range(len(self.pulsars))]
+        return self.finish(p, [q[0] for q in parts], [q[1] for q in parts])
 
 
 def _gauss_jordan(M):

@@ -27,8 +27,11 @@ def test_golden_vectors(require_gpu, name):
     check_parity(got, z["lnl_exact"], name + " vs extended precision", z["spread"], z["near"])
 
 
-@pytest.mark.parametrize("name", ["c2_small", "c3_small", "c4_small"])
+@pytest.mark.parametrize("name", ["c2_small", "c3_small", "c4_small", "c5_small", "c5_dipo"])
 def test_lds_kernel_matches_mfma_kernel(require_gpu, name):
+    """Kernel mode 1 (LDS Cholesky; for a correlated model the round-1 LDS
+    diagonal-block and LDS-staged panel kernels of the dense factorisation)
+    against the default register / MFMA kernels."""
     pta, z = load_golden(name, full=True)
     X = z["theta"]
     a = pta.get_lnlikelihood_batch(X)

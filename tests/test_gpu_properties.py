@@ -136,3 +136,33 @@ def test_graph_replay_matches_eager(require_gpu):
         np.testing.assert_array_equal(pta.get_lnlikelihood_batch(XX), ref[B])
     for i in range(16):                                   # single-theta calls (PTMCMC / bilby)
         assert pta.get_lnlikelihood(X[i]) == ref[16][i]
+
+
+def test_correlated_pulsar_partition(require_gpu):
+    """Config 5's model, one proposal over several devices (SURVEY.md §8(e)
+    exchange step): (1) a handle with 3 contexts and B < 3 splits the pulsars,
+    gathers the kept blocks peer-to-peer and finishes on the first context;
+    (2) the ABI protocol the torchrun ranks use -- ewh_corr_partial_device on
+    pulsar ranges into pulsar-major buffers, then ewh_corr_finish_device.
+    Both equal the one-device result bit for bit."""
+    import torch
+    c5 = synth.config_c5(n_psr=16, n_toa=800, seed=55, epoch_size=8)
+    pta = c5.pta
+    X = synth.near_draws(pta, c5.truth, 2, 57)
+    one = pta.get_lnlikelihood_batch(X)
+    pta.engine(devices=[0, 0, 0])
+    for B in (1, 2):
+        np.testing.assert_array_equal(pta.get_lnlikelihood_batch(X[:B]), one[:B])
+    eng = pta.engine(devices=[0])
+    kd = eng.keep_dim()
+    P, B = len(pta.signal_collections), len(X)
+    th = torch.from_numpy(X).cuda()
+    keep = torch.zeros((P, B, kd, kd), dtype=torch.float64, device="cuda")
+    local = torch.zeros((P, B), dtype=torch.float64, device="cuda")
+    out = torch.zeros(B, dtype=torch.float64, device="cuda")
+    s = torch.cuda.current_stream().cuda_stream
+    for p0, p1 in ((0, 5), (5, 11), (11, P)):
+        eng.corr_partial_device(th.data_ptr(), B, p0, p1, keep.data_ptr(), local.data_ptr(), s)
+    eng.corr_finish_device(th.data_ptr(), B, keep.data_ptr(), local.data_ptr(), out.data_ptr(), s)
+    torch.cuda.synchronize()
+    np.testing.assert_array_equal(out.cpu().numpy(), one)
