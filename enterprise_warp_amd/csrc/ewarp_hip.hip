@@ -727,6 +727,60 @@ __global__ __launch_bounds__(256) void dchol_rowupdate_kernel(double* __restrict
     for (int r = 0; r < 4; ++r) Aij[(long long)(16 * w + q + 4 * r) * Np + 16 * jb + c] = acc[jb][r];
 }
 
+// The same row update with more waves per CU (the default): only U_pj is
+// staged through LDS (one 64 x 64 tile, 33 KB: four workgroups fit a CU
+// instead of two); each wave reads its A operand -- the 64 x 16 column slab
+// of U_pi it multiplies, 16 doubles per lane -- straight from global memory
+// into registers, prefetched one step ahead together with the U_pj tile; the
+// minus sign is the MFMA neg modifier.  Same sums in the same order as
+// dchol_rowupdate_kernel: bit-identical.
+__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(4, 4)))
+void dchol_rowupdate2_kernel(double* __restrict__ mats, int Np, int i) {
+  __shared__ double Uj[DCB][DCB + 1];
+  const int j = i + blockIdx.x, bl = blockIdx.y, t = threadIdx.x;
+  double* base = mats + (long long)bl * Np * Np;
+  double* Aij = base + (long long)(DCB * i) * Np + DCB * j;
+  const int w = t >> 6, lane = t & 63, q = lane >> 4, c = lane & 15;
+  v4d acc[4];
+#pragma unroll
+  for (int jb = 0; jb < 4; ++jb)
+#pragma unroll
+    for (int r = 0; r < 4; ++r) acc[jb][r] = Aij[(long long)(16 * w + q + 4 * r) * Np + 16 * jb + c];
+  // A slab of U_pi (column block 16w..16w+15, all 64 rows): loaded at the top
+  // of step p, in flight across the LDS store and barriers; U_pj prefetched
+  // one step ahead into registers for the LDS store
+  const double* acol = base + DCB * i + 16 * w + c + (long long)q * Np;
+  const double* bcol = base + DCB * j + (t & 63) + (long long)(t >> 6) * Np;
+  double pb[16];
+  auto bload = [&](int p) {
+    const double* rp = bcol + (long long)(DCB * p) * Np;
+#pragma unroll
+    for (int r = 0; r < 16; ++r) pb[r] = rp[(long long)(4 * r) * Np];
+  };
+  if (i > 0) bload(0);
+  for (int p = 0; p < i; ++p) {
+    double a[16];
+    const double* ap = acol + (long long)(DCB * p) * Np;
+#pragma unroll
+    for (int ts = 0; ts < 16; ++ts) a[ts] = ap[(long long)(4 * ts) * Np];
+    __syncthreads();
+#pragma unroll
+    for (int r = 0; r < 16; ++r) Uj[(t >> 6) + 4 * r][t & 63] = pb[r];
+    __syncthreads();
+    if (p + 1 < i) bload(p + 1);
+#pragma unroll
+    for (int ts = 0; ts < DCB / 4; ++ts) {
+#pragma unroll
+      for (int jb = 0; jb < 4; ++jb)
+        acc[jb] = __builtin_amdgcn_mfma_f64_16x16x4f64(a[ts], Uj[4 * ts + q][16 * jb + c], acc[jb], 0, 0, 1);
+    }
+  }
+#pragma unroll
+  for (int jb = 0; jb < 4; ++jb)
+#pragma unroll
+    for (int r = 0; r < 4; ++r) Aij[(long long)(16 * w + q + 4 * r) * Np + 16 * jb + c] = acc[jb][r];
+}
+
 // ----------------------------------------------------------------------------
 // optimal statistic (EWH_COMMON_OPTSTAT handles; ewh_optstat)
 // From pulsar a's kept block K (its common columns G after eliminating the
@@ -1421,8 +1475,10 @@ int corr_finish(DevCtx* h, const double* theta_dev, int B, const double* keep, d
     EWH_HIP(hipMemsetAsync(h->d_cfail, 0, sizeof(int) * nb, st));
     for (int k = 0; k < nbk; ++k) {
       const int m = nbk - k - 1;
-      if (h->kernel_mode != 7 && k > 0)     // row-oriented update of block row k (default)
+      if (h->kernel_mode == 1 && k > 0)     // round-1 row update (both operands staged through LDS)
         hipLaunchKernelGGL(dchol_rowupdate_kernel, dim3(m + 1, nb), dim3(256), 0, st, h->d_dense, h->Np, k);
+      else if (h->kernel_mode != 7 && k > 0)   // row-oriented update of block row k (default)
+        hipLaunchKernelGGL(dchol_rowupdate2_kernel, dim3(m + 1, nb), dim3(256), 0, st, h->d_dense, h->Np, k);
       if (h->kernel_mode == 7 || h->kernel_mode == 1) {   // A/B: round-1 LDS diagonal block + LDS-staged panel
         hipLaunchKernelGGL(dchol_diag_kernel, dim3(nb), dim3(256), 0, st, h->d_dense, h->Np, k, h->d_wbuf,
                            h->d_cldet, h->d_cq, h->d_cfail);
