@@ -396,11 +396,14 @@ __global__ __launch_bounds__(256) void common_assemble_kernel(const double* __re
   double* row = mats + ((long long)bl * Np + i) * Np;
   const double* kb = keep + (long long)(b0 + bl) * KD * KD;
   const double* mb = minv + (long long)bl * nc * P * P;
+  // only the upper tiles (64-column tiles at or right of the diagonal tile)
+  // are ever read by the factorisation: the rest of the row is not written
+  const int j0 = (i / DCB) * DCB;
   if (i < N) {
     const int a = i / nc, g = i - a * nc;
     const double* ka = kb + (long long)a * ps + g * KD;            // row g of pulsar a's kept square
     const double* mg = mb + (long long)rep[g] * P * P + (long long)a * P;  // row a of M_g^-1
-    for (int j = threadIdx.x; j < Np; j += 256) {
+    for (int j = j0 + threadIdx.x; j < Np; j += 256) {
       double v = 0.0;
       if (j < N) {
         const int bb = j / nc, h = j - bb * nc;
@@ -412,7 +415,7 @@ __global__ __launch_bounds__(256) void common_assemble_kernel(const double* __re
       row[j] = v;
     }
   } else if (i == Np - 1) {
-    for (int j = threadIdx.x; j < Np; j += 256) {
+    for (int j = j0 + threadIdx.x; j < Np; j += 256) {
       double v = 0.0;
       if (j < N) {
         const int bb = j / nc, h = j - bb * nc;
@@ -423,7 +426,7 @@ __global__ __launch_bounds__(256) void common_assemble_kernel(const double* __re
       row[j] = v;
     }
   } else {
-    for (int j = threadIdx.x; j < Np; j += 256) row[j] = (j == i) ? 1.0 : 0.0;
+    for (int j = j0 + threadIdx.x; j < Np; j += 256) row[j] = (j == i) ? 1.0 : 0.0;
   }
 }
 
@@ -779,6 +782,79 @@ void dchol_rowupdate2_kernel(double* __restrict__ mats, int Np, int i) {
   for (int jb = 0; jb < 4; ++jb)
 #pragma unroll
     for (int r = 0; r < 4; ++r) Aij[(long long)(16 * w + q + 4 * r) * Np + 16 * jb + c] = acc[jb][r];
+}
+
+// Row update + panel in one pass for the tiles j > k of block row k (after
+// dchol_diag_reg_kernel has factored tile (k, k)): wave w owns the 16-column
+// strip w of tile (k, j) over all 64 rows, so after accumulating
+// A_kj - sum_p U_pk^T U_pj it applies the block forward substitution of
+// dchol_panel_reg_kernel to its own registers and writes U_kj once (no
+// round trip of the updated tile through HBM, one launch less per block row).
+// U_pk is staged through LDS (shared by the four waves), each wave's U_pj
+// slab comes from global memory into registers.  Same sums, same order as
+// dchol_rowupdate2_kernel + dchol_panel_reg_kernel: bit-identical.
+__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(3, 3)))
+void dchol_rowpanel_kernel(double* __restrict__ mats, int Np, int k, const double* __restrict__ wbuf) {
+  __shared__ double Uk[DCB][DCB + 1];
+  const int j = k + 1 + blockIdx.x, bl = blockIdx.y, t = threadIdx.x;
+  double* base = mats + (long long)bl * Np * Np;
+  double* Akj = base + (long long)(DCB * k) * Np + DCB * j;
+  const int w = t >> 6, lane = t & 63, q = lane >> 4, c = lane & 15;
+  v4d acc[4];
+#pragma unroll
+  for (int s0 = 0; s0 < 4; ++s0)
+#pragma unroll
+    for (int r = 0; r < 4; ++r) acc[s0][r] = Akj[(long long)(16 * s0 + q + 4 * r) * Np + 16 * w + c];
+  const double* bcol = base + DCB * j + 16 * w + c + (long long)q * Np;
+  const double* acol = base + DCB * k + (t & 63) + (long long)(t >> 6) * Np;
+  double pa[16];
+  auto aload = [&](int p) {
+    const double* rp = acol + (long long)(DCB * p) * Np;
+#pragma unroll
+    for (int r = 0; r < 16; ++r) pa[r] = rp[(long long)(4 * r) * Np];
+  };
+  if (k > 0) aload(0);
+  for (int p = 0; p < k; ++p) {
+    double b[16];
+    const double* bp = bcol + (long long)(DCB * p) * Np;
+#pragma unroll
+    for (int ts = 0; ts < 16; ++ts) b[ts] = bp[(long long)(4 * ts) * Np];
+    __syncthreads();
+#pragma unroll
+    for (int r = 0; r < 16; ++r) Uk[(t >> 6) + 4 * r][t & 63] = pa[r];
+    __syncthreads();
+    if (p + 1 < k) aload(p + 1);
+#pragma unroll
+    for (int ts = 0; ts < DCB / 4; ++ts) {
+#pragma unroll
+      for (int s0 = 0; s0 < 4; ++s0)
+        acc[s0] = __builtin_amdgcn_mfma_f64_16x16x4f64(Uk[4 * ts + q][16 * s0 + c], b[ts], acc[s0], 0, 0, 1);
+    }
+  }
+  // the panel: U_kj = L_kk^-1 A_kj on this strip (dchol_panel_reg_kernel)
+  const double* W = wbuf + (long long)bl * DW_SLOTS * 256 + lane * 4;
+  static_for<0, 4>([&](auto SS) {
+    constexpr int s0 = decltype(SS)::value;
+    static_for<0, s0>([&](auto TT) {
+      constexpr int t0 = decltype(TT)::value;
+      syrk_update(acc[s0], *(const v4d*)(W + dw_u(t0, s0) * 256), acc[t0]);
+    });
+    const v4d E = *(const v4d*)(W + s0 * 256);
+    const v4d rs = *(const v4d*)(W + (4 + s0) * 256);
+    v4d v = {0.0, 0.0, 0.0, 0.0};
+    static_for<0, 4>([&](auto S2) {
+      constexpr int sk = decltype(S2)::value;
+      v = __builtin_amdgcn_mfma_f64_16x16x4f64(E[sk], acc[s0][sk], v, 0, 0, 0);
+    });
+    static_for<0, 4>([&](auto R) {
+      constexpr int r = decltype(R)::value;
+      acc[s0][r] = v[r] * rs[r];
+    });
+  });
+#pragma unroll
+  for (int s0 = 0; s0 < 4; ++s0)
+#pragma unroll
+    for (int r = 0; r < 4; ++r) Akj[(long long)(16 * s0 + q + 4 * r) * Np + 16 * w + c] = acc[s0][r];
 }
 
 // ----------------------------------------------------------------------------
@@ -1475,10 +1551,16 @@ int corr_finish(DevCtx* h, const double* theta_dev, int B, const double* keep, d
     EWH_HIP(hipMemsetAsync(h->d_cfail, 0, sizeof(int) * nb, st));
     for (int k = 0; k < nbk; ++k) {
       const int m = nbk - k - 1;
+      // default for large sample chunks: row update + panel fused (the updated
+      // tile never round-trips through HBM); small chunks (one PTMCMC
+      // proposal) keep the row update of every tile in one launch, which
+      // shortens the dependent chain per block row
+      const bool fused = h->kernel_mode != 1 && h->kernel_mode != 7 && nb >= 64;
       if (h->kernel_mode == 1 && k > 0)     // round-1 row update (both operands staged through LDS)
         hipLaunchKernelGGL(dchol_rowupdate_kernel, dim3(m + 1, nb), dim3(256), 0, st, h->d_dense, h->Np, k);
-      else if (h->kernel_mode != 7 && k > 0)   // row-oriented update of block row k (default)
-        hipLaunchKernelGGL(dchol_rowupdate2_kernel, dim3(m + 1, nb), dim3(256), 0, st, h->d_dense, h->Np, k);
+      else if (k > 0 && h->kernel_mode != 7)   // the diagonal tile's row update only (fused), or the whole row
+        hipLaunchKernelGGL(dchol_rowupdate2_kernel, dim3(fused ? 1 : m + 1, nb), dim3(256), 0, st, h->d_dense, h->Np,
+                           k);
       if (h->kernel_mode == 7 || h->kernel_mode == 1) {   // A/B: round-1 LDS diagonal block + LDS-staged panel
         hipLaunchKernelGGL(dchol_diag_kernel, dim3(nb), dim3(256), 0, st, h->d_dense, h->Np, k, h->d_wbuf,
                            h->d_cldet, h->d_cq, h->d_cfail);
@@ -1491,7 +1573,9 @@ int corr_finish(DevCtx* h, const double* theta_dev, int B, const double* keep, d
         else
           hipLaunchKernelGGL(HIP_KERNEL_NAME(dchol_diag_reg_kernel<true>), dim3(nb), dim3(64), 0, st, h->d_dense,
                              h->Np, k, h->d_wbuf, h->d_cldet, h->d_cq, h->d_cfail);
-        if (m > 0)
+        if (m > 0 && fused)
+          hipLaunchKernelGGL(dchol_rowpanel_kernel, dim3(m, nb), dim3(256), 0, st, h->d_dense, h->Np, k, h->d_wbuf);
+        else if (m > 0)
           hipLaunchKernelGGL(dchol_panel_reg_kernel, dim3(4 * m, nb), dim3(64), 0, st, h->d_dense, h->Np, k,
                              h->d_wbuf);
       }
