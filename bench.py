@@ -168,7 +168,15 @@ def main():
                     help="c5 only: shard samples (no exchange) or pulsars (all-gather of the kept common blocks, "
                          "then the dense factorisation on every rank: one proposal over N GPUs)")
     ap.add_argument("--c5-batch", type=int, default=None, help="c5 proposals per step (default 512 / 1 for pulsars)")
+    ap.add_argument("--dist-backend", default="nccl", choices=["nccl", "gloo"],
+                    help="nccl (= RCCL, the default); gloo only to rehearse the multi-rank path")
+    ap.add_argument("--same-device", action="store_true",
+                    help="every rank on cuda:0 (rehearsal on a one-GPU box; needs --dist-backend gloo)")
+    ap.add_argument("--verify", action="store_true",
+                    help="rank 0 checks the reduced lnL of the first samples against the single-device entry")
     args = ap.parse_args()
+    if args.same_device and args.dist_backend != "gloo":
+        ap.error("--same-device needs --dist-backend gloo (RCCL takes one rank per GPU)")
     if args.config == "c5":
         return main_c5(args)
 
@@ -184,12 +192,18 @@ def main():
     cpu = None
     if world == 1 and not args.no_cpu_baseline:
         cpu = cpu_baseline(args.cpu_seconds, args.cpu_procs)
+    # --same-device (rehearsal of the multi-rank path on a one-GPU box, with
+    # --dist-backend gloo): every rank on cuda:0
+    gpu = 0 if (world == 1 or args.same_device) else local
     if world > 1:
-        torch.cuda.set_device(local)
-        dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+        torch.cuda.set_device(gpu)
+        if args.dist_backend == "nccl":
+            dist.init_process_group("nccl", device_id=torch.device("cuda", gpu))
+        else:
+            dist.init_process_group(args.dist_backend)
     else:
         torch.cuda.set_device(0)
-    dev = torch.device("cuda", local if world > 1 else 0)
+    dev = torch.device("cuda", gpu)
 
     cfg = synth.config_c3()
     pta = cfg.pta
@@ -200,16 +214,36 @@ def main():
     eng.set_kernel_mode(args.kernel_mode)
     costs = eng.unit_costs()
     u0, u1 = sharding.unit_ranges(costs, B, world)[rank]
-    out = torch.zeros(B, dtype=torch.float64, device=dev)
     stream = torch.cuda.current_stream(dev)
+    # two output buffers: the all-reduce of step i (RCCL's stream) overlaps
+    # the likelihood launch of step i+1 (this stream); step i+2 reuses the
+    # buffer only after that all-reduce (work.wait(): a stream dependency for
+    # RCCL, not a host wait)
+    outs = [torch.zeros(B, dtype=torch.float64, device=dev) for _ in range(2)]
+    works = [None, None]
 
-    def step():
-        eng.lnl_units_device(theta.data_ptr(), B, u0, u1, out.data_ptr(), stream.cuda_stream)
+    def step(i, ev=None):
+        k = i & 1
+        if works[k] is not None:
+            works[k].wait()
+            works[k] = None
+        if ev is not None:
+            ev[0].record(stream)
+        eng.lnl_units_device(theta.data_ptr(), B, u0, u1, outs[k].data_ptr(), stream.cuda_stream)
+        if ev is not None:
+            ev[1].record(stream)
         if world > 1:
-            dist.all_reduce(out)
+            works[k] = dist.all_reduce(outs[k], async_op=True)
 
-    for _ in range(args.warmup):
-        step()
+    def drain():
+        for k in range(2):
+            if works[k] is not None:
+                works[k].wait()
+                works[k] = None
+
+    for i in range(args.warmup):
+        step(i)
+    drain()
     torch.cuda.synchronize(dev)
     if world > 1:
         dist.barrier()
@@ -217,11 +251,8 @@ def main():
     ev = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)) for _ in range(args.steps)]
     t0 = time.perf_counter()
     for i in range(args.steps):
-        ev[i][0].record(stream)
-        eng.lnl_units_device(theta.data_ptr(), B, u0, u1, out.data_ptr(), stream.cuda_stream)
-        ev[i][1].record(stream)
-        if world > 1:
-            dist.all_reduce(out)
+        step(i, ev[i])
+    drain()
     torch.cuda.synchronize(dev)
     if world > 1:
         dist.barrier()
@@ -232,7 +263,18 @@ def main():
     if world > 1:
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
     elapsed = float(t.item())
-    lnl = out.cpu().numpy()
+    lnl = outs[(args.steps - 1) & 1].cpu().numpy()
+    verify = None
+    if args.verify and rank == 0:
+        # the reduced batch against the single-device entry (ewh_lnl_batch,
+        # pulsar-order device fold) on its first samples: strict bound
+        nv = min(B, 256)
+        ref = pta.get_lnlikelihood_batch(X[:nv])
+        fin = np.isfinite(ref)
+        same_inf = bool(np.array_equal(fin, np.isfinite(lnl[:nv])))
+        err = np.abs(lnl[:nv][fin] - ref[fin]) / (1e-6 + 1e-10 * np.abs(ref[fin]))
+        verify = {"samples": nv, "max_err_over_strict": float(err.max()) if err.size else 0.0,
+                  "inf_pattern_equal": same_inf}
 
     # roofline of the dominant kernel (chol_mfma): algorithmic flops of this
     # rank's units / average duration of its likelihood launch
@@ -271,11 +313,13 @@ def main():
         if cpu is not None:
             rec["cpu_baseline"] = cpu
             rec["gpu_over_cpu"] = {"per_gpu": value / world / cpu["value"],
-                                   "node_8gpu_projected_at_this_per_gpu_rate": 8 * value / world / cpu["value"],
-                                   "note": "projection assumes perfect weak scaling to 8 GPUs against this host's "
-                                           "usable cores; SCALE_rNN measures the real curve"}
+                                   "note": "one GPU against the CPU cores this job is given (its node share); "
+                                           "a whole node is 8 such shares, so the node-level ratio at perfect "
+                                           "scaling is the same figure (SCALE_rNN measures the real curve)"}
         if latency is not None:
             rec["sampler_latency"] = latency
+        if verify is not None:
+            rec["verify"] = verify
         print(json.dumps(rec), flush=True)
     if world > 1:
         dist.destroy_process_group()
