@@ -39,7 +39,7 @@ int dispatch_contract(int nb, const PsrDev& P, const double* w, const double* be
 template <int NB>
 int launch_contract2(const PsrDev& P, const double* w, const double* beta, double* s, long long s_stride, double* G,
                      int nb_samples, hipStream_t st) {
-  const size_t lds = (size_t)(2 * CT_ROWS * 16 * NB + 3 * CT_ROWS) * sizeof(double);
+  const size_t lds = (size_t)(2 * CT_ROWS * 16 * NB + 6 * CT_ROWS) * sizeof(double);
   // (the dynamic-LDS attribute is set per device by set_contract_attributes)
   hipLaunchKernelGGL(HIP_KERNEL_NAME(contract2_kernel<NB>), dim3(nb_samples), dim3(256), lds, st, P, w, beta, s,
                      s_stride, G);
@@ -68,7 +68,7 @@ int dispatch_contract2(int nb, const PsrDev& P, const double* w, const double* b
 
 template <int NB>
 int set_attr2() {
-  const size_t lds = (size_t)(2 * CT_ROWS * 16 * NB + 3 * CT_ROWS) * sizeof(double);
+  const size_t lds = (size_t)(2 * CT_ROWS * 16 * NB + 6 * CT_ROWS) * sizeof(double);
   EWH_HIP(hipFuncSetAttribute((const void*)contract2_kernel<NB>, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds));
   return 0;
 }

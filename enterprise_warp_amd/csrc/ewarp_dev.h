@@ -371,10 +371,13 @@ __device__ __forceinline__ void contract2_body(const PsrDev& P, const double* __
   constexpr int TILE = CT_ROWS * LD;                 // doubles per tile
   constexpr int CHUNKS = TILE * 8 / 1024 / 4;        // 1-KiB glds pieces per wave per tile (= NB)
   static_assert(CHUNKS * 4 * 1024 == TILE * 8, "tile must split into 4 x NB pieces of 1 KiB");
-  // LDS: [2][TILE] tiles | [2][CT_ROWS] weights | [2][CT_ROWS] int epoch flags
+  // LDS: [2][TILE] tiles | [2][CT_ROWS] weights | [2][CT_ROWS] epoch-sum
+  // weights | [2][CT_ROWS] int flush epoch ids | [2] int flush masks
   const int tid = threadIdx.x, lane = tid & 63, q = lane >> 4, c = lane & 15;
   double* const wbase = smem + 2 * TILE;
-  int* const ebase = (int*)(smem + 2 * TILE + 2 * CT_ROWS);
+  double* const ewbase = wbase + 2 * CT_ROWS;
+  int* const ebase = (int*)(ewbase + 2 * CT_ROWS);
+  int* const fmbase = ebase + 2 * CT_ROWS;
 
   v4d acc[SLOTS > 0 ? SLOTS : 1];
 #pragma unroll
@@ -384,6 +387,7 @@ __device__ __forceinline__ void contract2_body(const PsrDev& P, const double* __
   double eacc = 0.0;                                 // running s_e of column `tid`
   // pass 0: TOA rows (weights w); pass 1: epoch rows (weights -beta)
   for (int pass = 0; pass < (ecorr ? 2 : 1); ++pass) {
+    const bool epochs = pass == 0 && ecorr;
     const int nrows = pass == 0 ? P.n_toa : P.n_epoch;
     const double* src = pass == 0 ? P.T : srow;
     const double* wsrc = pass == 0 ? wrow : brow;
@@ -396,25 +400,47 @@ __device__ __forceinline__ void contract2_body(const PsrDev& P, const double* __
       for (int k = 0; k < CHUNKS; ++k)
         __builtin_amdgcn_global_load_lds((gbl_void_t*)(g + k * 1024), (lds_void_t*)(l + k * 1024), 16, 0, 0);
     };
-    double wv = 0.0;
+    // the tile's weights and epoch flags: wave 0 only (a compile-time branch,
+    // no exec mask), loaded unconditionally from a clamped index and BEFORE
+    // the tile's global_load_lds, so the wait for them is a counted vmcnt at
+    // their use (the LDS store at the end of the iteration), never a
+    // vmcnt(0) that would also wait for the next tile's DMA
+    double wraw = 0.0;
     int ev = -1;
     auto small = [&](int it) {
-      const int t = it * CT_ROWS + tid;
-      wv = (tid < CT_ROWS && t < nrows) ? wsign * wsrc[t] : 0.0;
-      ev = (pass == 0 && tid < CT_ROWS) ? P.toa_ep[t] : -1;
+      if constexpr (WAVE == 0) {
+        const int t = it * CT_ROWS + (lane & (CT_ROWS - 1));
+        wraw = wsrc[min(t, nrows - 1)];
+        ev = pass == 0 ? P.toa_ep[t] : -1;
+      }
     };
-    issue(0);
+    // staged per tile by wave 0: the Gram weights; the epoch-sum weights
+    // (w on rows inside an epoch, 0 elsewhere); the mask of rows that close
+    // an epoch and, in mask order, the epochs they close.  The epoch-sum loop
+    // then runs on registers and one scalar mask: no per-row LDS round trip.
+    auto stage = [&](int buf, int it) {
+      if constexpr (WAVE == 0) {
+        const int t = it * CT_ROWS + lane;
+        const double w = (lane < CT_ROWS && t < nrows) ? wsign * wraw : 0.0;
+        const bool fl = lane < CT_ROWS && ev >= 0 && (ev & 1);
+        const unsigned long long fmask = __ballot(fl);
+        if (lane < CT_ROWS) {
+          wbase[buf * CT_ROWS + lane] = w;
+          ewbase[buf * CT_ROWS + lane] = ev >= 0 ? w : 0.0;
+        }
+        if (fl) ebase[buf * CT_ROWS + __builtin_amdgcn_mbcnt_lo((unsigned)fmask, 0u)] = ev >> 1;
+        if (lane == 0) fmbase[buf] = (int)(unsigned)fmask;
+      }
+    };
     small(0);
-    if (tid < CT_ROWS) {
-      wbase[tid] = wv;
-      ebase[tid] = ev;
-    }
+    issue(0);
+    stage(0, 0);
     __syncthreads();
     for (int it = 0; it < ntile; ++it) {
       const int cur = it & 1;
       if (it + 1 < ntile) {
-        issue(it + 1);
         small(it + 1);
+        issue(it + 1);
       }
       const double* tile = smem + cur * TILE;
       const double* wt = wbase + cur * CT_ROWS;
@@ -435,32 +461,39 @@ __device__ __forceinline__ void contract2_body(const PsrDev& P, const double* __
           acc[decltype(SL)::value] = __builtin_amdgcn_mfma_f64_16x16x4f64(av[bi], tv[bj], acc[decltype(SL)::value], 0, 0, 0);
         });
       }
-      if (pass == 0 && ecorr && tid < LD) {          // epoch sums of column tid
-        // the tile's 32 values of the column are read up front (independent
-        // LDS loads, one round trip) and the epoch flags are wave-uniform
-        // (readfirstlane: scalar branches), so the running sum is a chain of
-        // FMAs instead of a dependent LDS read + branch per row
+      if (epochs && tid < LD) {                      // epoch sums of column tid
+        // rows outside an epoch carry weight 0 (T is finite: fma(0, t, s) = s
+        // exactly), so the running sum is a plain FMA chain over the tile,
+        // its operands read 8 rows per LDS round trip; a row that closes an
+        // epoch (bit of the wave-uniform mask) stores the sum and resets it.
+        // (Interleaving the chain with the k-steps' MFMAs measured no faster
+        // on C2 and 5 % slower on C4: more live registers.)
         const double* tcol = tile + tid;
-        const int* ecur = ebase + cur * CT_ROWS;
-        double tc[CT_ROWS];
+        const double* ew = ewbase + cur * CT_ROWS;
+        const int* fe = ebase + cur * CT_ROWS;
+        const unsigned fm = (unsigned)__builtin_amdgcn_readfirstlane(fmbase[cur]);
+        int nf = 0;
 #pragma unroll
-        for (int r = 0; r < CT_ROWS; ++r) tc[r] = tcol[r * LD];
+        for (int r0 = 0; r0 < CT_ROWS; r0 += 8) {
+          double tc[8], wc[8];
 #pragma unroll
-        for (int r = 0; r < CT_ROWS; ++r) {
-          const int e = __builtin_amdgcn_readfirstlane(ecur[r]);
-          if (e >= 0) {
-            eacc = fma(wt[r], tc[r], eacc);
-            if (e & 1) {
-              srow[(long long)(e >> 1) * LD + tid] = eacc;
+          for (int i = 0; i < 8; ++i) {
+            tc[i] = tcol[(r0 + i) * LD];
+            wc[i] = ew[r0 + i];
+          }
+#pragma unroll
+          for (int i = 0; i < 8; ++i) {
+            eacc = fma(wc[i], tc[i], eacc);
+            if ((fm >> (r0 + i)) & 1u) {
+              const int e = __builtin_amdgcn_readfirstlane(fe[nf]);
+              srow[(long long)e * LD + tid] = eacc;
               eacc = 0.0;
+              ++nf;
             }
           }
         }
       }
-      if (it + 1 < ntile && tid < CT_ROWS) {
-        wbase[(cur ^ 1) * CT_ROWS + tid] = wv;
-        ebase[(cur ^ 1) * CT_ROWS + tid] = ev;
-      }
+      if (it + 1 < ntile) stage(cur ^ 1, it + 1);
       __syncthreads();                               // drains the glds of tile it+1 (vmcnt(0))
     }
     if (pass == 0 && ecorr && tid < LD) {
