@@ -36,40 +36,42 @@ int dispatch_contract(int nb, const PsrDev& P, const double* w, const double* be
   return 0;
 }
 
+constexpr size_t contract2_lds(int nb) { return (size_t)(2 * CT_ROWS * 16 * nb + 6 * CT_ROWS) * sizeof(double); }
+
+// waves per sample: 4, or 8 where measured faster (fewer accumulators per
+// wave: more waves per SIMD to hide the k-steps' LDS latency)
+constexpr int contract2_default_waves(int nb) { return nb >= 9 ? 8 : 4; }
+
 template <int NB>
-int launch_contract2(const PsrDev& P, const double* w, const double* beta, double* s, long long s_stride, double* G,
-                     int nb_samples, hipStream_t st) {
-  const size_t lds = (size_t)(2 * CT_ROWS * 16 * NB + 6 * CT_ROWS) * sizeof(double);
+int launch_contract2(int waves, const PsrDev& P, const double* w, const double* beta, double* s, long long s_stride,
+                     double* G, int nb_samples, hipStream_t st) {
   // (the dynamic-LDS attribute is set per device by set_contract_attributes)
-  hipLaunchKernelGGL(HIP_KERNEL_NAME(contract2_kernel<NB>), dim3(nb_samples), dim3(256), lds, st, P, w, beta, s,
-                     s_stride, G);
+  if (waves == 0) waves = contract2_default_waves(NB);
+  if (waves == 8)
+    hipLaunchKernelGGL(HIP_KERNEL_NAME(contract2_kernel<NB, 8>), dim3(nb_samples), dim3(512), contract2_lds(NB), st, P,
+                       w, beta, s, s_stride, G);
+  else
+    hipLaunchKernelGGL(HIP_KERNEL_NAME(contract2_kernel<NB, 4>), dim3(nb_samples), dim3(256), contract2_lds(NB), st, P,
+                       w, beta, s, s_stride, G);
   return 0;
 }
 
-int dispatch_contract2(int nb, const PsrDev& P, const double* w, const double* beta, double* s, long long s_stride,
-                       double* G, int nb_samples, hipStream_t st) {
-  switch (nb) {
-    case 1: return launch_contract2<1>(P, w, beta, s, s_stride, G, nb_samples, st);
-    case 2: return launch_contract2<2>(P, w, beta, s, s_stride, G, nb_samples, st);
-    case 3: return launch_contract2<3>(P, w, beta, s, s_stride, G, nb_samples, st);
-    case 4: return launch_contract2<4>(P, w, beta, s, s_stride, G, nb_samples, st);
-    case 5: return launch_contract2<5>(P, w, beta, s, s_stride, G, nb_samples, st);
-    case 6: return launch_contract2<6>(P, w, beta, s, s_stride, G, nb_samples, st);
-    case 7: return launch_contract2<7>(P, w, beta, s, s_stride, G, nb_samples, st);
-    case 8: return launch_contract2<8>(P, w, beta, s, s_stride, G, nb_samples, st);
-    case 9: return launch_contract2<9>(P, w, beta, s, s_stride, G, nb_samples, st);
-    case 10: return launch_contract2<10>(P, w, beta, s, s_stride, G, nb_samples, st);
-    case 11: return launch_contract2<11>(P, w, beta, s, s_stride, G, nb_samples, st);
-    case 12: return launch_contract2<12>(P, w, beta, s, s_stride, G, nb_samples, st);
-    case 13: return launch_contract2<13>(P, w, beta, s, s_stride, G, nb_samples, st);
-    default: return set_err(EWH_E_UNSUPPORTED, "basis too wide for the pipelined contraction (> 207 columns)");
-  }
+int dispatch_contract2(int nb, int waves, const PsrDev& P, const double* w, const double* beta, double* s,
+                       long long s_stride, double* G, int nb_samples, hipStream_t st) {
+  int rc = 1;
+  static_for<1, CONTRACT2_NB_MAX + 1>([&](auto N) {
+    if (nb == decltype(N)::value) rc = launch_contract2<decltype(N)::value>(waves, P, w, beta, s, s_stride, G, nb_samples, st);
+  });
+  if (rc == 1) return set_err(EWH_E_UNSUPPORTED, "basis too wide for the pipelined contraction (> 207 columns)");
+  return rc;
 }
 
 template <int NB>
 int set_attr2() {
-  const size_t lds = (size_t)(2 * CT_ROWS * 16 * NB + 6 * CT_ROWS) * sizeof(double);
-  EWH_HIP(hipFuncSetAttribute((const void*)contract2_kernel<NB>, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds));
+  EWH_HIP(hipFuncSetAttribute((const void*)contract2_kernel<NB, 4>, hipFuncAttributeMaxDynamicSharedMemorySize,
+                              (int)contract2_lds(NB)));
+  EWH_HIP(hipFuncSetAttribute((const void*)contract2_kernel<NB, 8>, hipFuncAttributeMaxDynamicSharedMemorySize,
+                              (int)contract2_lds(NB)));
   return 0;
 }
 
@@ -100,9 +102,9 @@ int launch_contract_nb(int nb, const PsrDev& P, const double* w, const double* b
   return dispatch_contract(nb, P, w, beta, s, fac, G, nb_samples, st);
 }
 
-int launch_contract2_nb(int nb, const PsrDev& P, const double* w, const double* beta, double* s,
+int launch_contract2_nb(int nb, int waves, const PsrDev& P, const double* w, const double* beta, double* s,
                         long long s_stride, double* G, int nb_samples, hipStream_t st) {
-  return dispatch_contract2(nb, P, w, beta, s, s_stride, G, nb_samples, st);
+  return dispatch_contract2(nb, waves, P, w, beta, s, s_stride, G, nb_samples, st);
 }
 
 }  // namespace ewh_dev

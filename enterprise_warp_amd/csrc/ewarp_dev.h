@@ -348,29 +348,29 @@ constexpr int tri_j(int nb, int blk) {
   while (blk >= nb - i) { blk -= nb - i; ++i; }
   return i + blk;
 }
-// does wave `wave` (blocks wave + 4 sl) touch block column j as a row (A) / at all?
-constexpr bool wave_uses_row(int nb, int wave, int j) {
-  for (int blk = wave; blk < nb * (nb + 1) / 2; blk += 4)
+// does wave `wave` of W (blocks wave + W sl) touch block column j as a row (A) / at all?
+constexpr bool wave_uses_row(int nb, int wave, int j, int W = 4) {
+  for (int blk = wave; blk < nb * (nb + 1) / 2; blk += W)
     if (tri_i(nb, blk) == j) return true;
   return false;
 }
-constexpr bool wave_uses(int nb, int wave, int j) {
-  for (int blk = wave; blk < nb * (nb + 1) / 2; blk += 4)
+constexpr bool wave_uses(int nb, int wave, int j, int W = 4) {
+  for (int blk = wave; blk < nb * (nb + 1) / 2; blk += W)
     if (tri_i(nb, blk) == j || tri_j(nb, blk) == j) return true;
   return false;
 }
 
-template <int NB, int WAVE>
+template <int NB, int WAVE, int W>
 __device__ __forceinline__ void contract2_body(const PsrDev& P, const double* __restrict__ wrow,
                                                const double* __restrict__ brow, double* __restrict__ srow,
                                                double* __restrict__ Gout) {
   extern __shared__ __attribute__((aligned(16))) double smem[];
   constexpr int LD = 16 * NB;
   constexpr int NBLK = NB * (NB + 1) / 2;
-  constexpr int SLOTS = (NBLK - WAVE + 3) / 4;
+  constexpr int SLOTS = (NBLK - WAVE + W - 1) / W;
   constexpr int TILE = CT_ROWS * LD;                 // doubles per tile
-  constexpr int CHUNKS = TILE * 8 / 1024 / 4;        // 1-KiB glds pieces per wave per tile (= NB)
-  static_assert(CHUNKS * 4 * 1024 == TILE * 8, "tile must split into 4 x NB pieces of 1 KiB");
+  constexpr int CHUNKS = TILE * 8 / 1024;            // 1-KiB glds pieces per tile (4 NB), dealt round-robin to the W waves
+  static_assert(CHUNKS * 1024 == TILE * 8, "tile must split into pieces of 1 KiB");
   // LDS: [2][TILE] tiles | [2][CT_ROWS] weights | [2][CT_ROWS] epoch-sum
   // weights | [2][CT_ROWS] int flush epoch ids | [2] int flush masks
   const int tid = threadIdx.x, lane = tid & 63, q = lane >> 4, c = lane & 15;
@@ -394,10 +394,10 @@ __device__ __forceinline__ void contract2_body(const PsrDev& P, const double* __
     const double wsign = pass == 0 ? 1.0 : -1.0;
     const int ntile = (nrows + CT_ROWS - 1) / CT_ROWS;
     auto issue = [&](int it) {
-      const char* g = (const char*)(src + (long long)it * TILE) + (WAVE * CHUNKS) * 1024 + lane * 16;
-      char* l = (char*)(smem + (it & 1) * TILE) + (WAVE * CHUNKS) * 1024;
+      const char* g = (const char*)(src + (long long)it * TILE) + lane * 16;
+      char* l = (char*)(smem + (it & 1) * TILE);
 #pragma unroll
-      for (int k = 0; k < CHUNKS; ++k)
+      for (int k = WAVE; k < CHUNKS; k += W)
         __builtin_amdgcn_global_load_lds((gbl_void_t*)(g + k * 1024), (lds_void_t*)(l + k * 1024), 16, 0, 0);
     };
     // the tile's weights and epoch flags: wave 0 only (a compile-time branch,
@@ -452,11 +452,11 @@ __device__ __forceinline__ void contract2_body(const PsrDev& P, const double* __
         double tv[NB], av[NB];
         static_for<0, NB>([&](auto J) {
           constexpr int j = decltype(J)::value;
-          if constexpr (wave_uses(NB, WAVE, j)) tv[j] = trow[16 * j];
-          if constexpr (wave_uses_row(NB, WAVE, j)) av[j] = wr * tv[j];
+          if constexpr (wave_uses(NB, WAVE, j, W)) tv[j] = trow[16 * j];
+          if constexpr (wave_uses_row(NB, WAVE, j, W)) av[j] = wr * tv[j];
         });
         static_for<0, SLOTS>([&](auto SL) {
-          constexpr int blk = WAVE + 4 * decltype(SL)::value;
+          constexpr int blk = WAVE + W * decltype(SL)::value;
           constexpr int bi = tri_i(NB, blk), bj = tri_j(NB, blk);
           acc[decltype(SL)::value] = __builtin_amdgcn_mfma_f64_16x16x4f64(av[bi], tv[bj], acc[decltype(SL)::value], 0, 0, 0);
         });
@@ -509,7 +509,7 @@ __device__ __forceinline__ void contract2_body(const PsrDev& P, const double* __
   // epilogue: C/D layout lane -> (row q + 4r, col c); mirror to the lower half,
   // unit diagonal on pad columns (m .. LD-2) so they factor as identity.
   static_for<0, SLOTS>([&](auto SL) {
-    constexpr int blk = WAVE + 4 * decltype(SL)::value;
+    constexpr int blk = WAVE + W * decltype(SL)::value;
     constexpr int bi = tri_i(NB, blk), bj = tri_j(NB, blk);
 #pragma unroll
     for (int r = 0; r < 4; ++r) {
@@ -522,22 +522,22 @@ __device__ __forceinline__ void contract2_body(const PsrDev& P, const double* __
   });
 }
 
-template <int NB>
-__global__ __launch_bounds__(256) void contract2_kernel(PsrDev P, const double* __restrict__ w,
-                                                        const double* __restrict__ beta, double* __restrict__ s,
-                                                        long long s_stride, double* __restrict__ G) {
+// W = 4 or 8 waves per sample (8: half the accumulators per wave, so the
+// narrow NB = 9 kernel fits 4 waves per SIMD and the wide NB = 13 one 2)
+template <int NB, int W>
+__global__ __launch_bounds__(64 * W) void contract2_kernel(PsrDev P, const double* __restrict__ w,
+                                                           const double* __restrict__ beta, double* __restrict__ s,
+                                                           long long s_stride, double* __restrict__ G) {
   constexpr int LD = 16 * NB;
   const int bl = blockIdx.x;
   const double* wrow = w + (long long)bl * P.n_toa;
   const double* brow = beta + (long long)bl * P.n_epoch;
   double* srow = s + (long long)bl * s_stride;
   double* Gout = G + (long long)bl * LD * LD;
-  switch (threadIdx.x >> 6) {
-    case 0: contract2_body<NB, 0>(P, wrow, brow, srow, Gout); break;
-    case 1: contract2_body<NB, 1>(P, wrow, brow, srow, Gout); break;
-    case 2: contract2_body<NB, 2>(P, wrow, brow, srow, Gout); break;
-    default: contract2_body<NB, 3>(P, wrow, brow, srow, Gout); break;
-  }
+  const int wv = threadIdx.x >> 6;
+  static_for<0, W>([&](auto WV) {
+    if (wv == decltype(WV)::value) contract2_body<NB, decltype(WV)::value, W>(P, wrow, brow, srow, Gout);
+  });
 }
 
 // ----------------------------------------------------------------------------
@@ -1222,7 +1222,8 @@ constexpr int DCB = 64;            // dense panel width
 // each returns 0 on success (negative EWH_E* on error)
 int launch_contract_nb(int nb, const PsrDev& P, const double* w, const double* beta, const double* s,
                        const double* fac, double* G, int nb_samples, hipStream_t st);
-int launch_contract2_nb(int nb, const PsrDev& P, const double* w, const double* beta, double* s,
+// waves: 4 or 8 per sample (0 = the measured default for nb)
+int launch_contract2_nb(int nb, int waves, const PsrDev& P, const double* w, const double* beta, double* s,
                         long long s_stride, double* G, int nb_samples, hipStream_t st);
 // mode: ewh_set_kernel_mode; returns 1 if no register kernel applies (caller falls back)
 int launch_chol_small(int mode, int nb, const CholJob* jobs, int B, long long u0, long long n, int b_off,
@@ -1234,7 +1235,7 @@ int launch_partial_nb(int nb, int keep, const CholJob* jobs, int B, long long u0
                       const double* theta, int ldth, double* units, double* keep_out, int keep_bs, hipStream_t st);
 // dynamic-LDS attributes of the contraction kernels on the current device
 int set_contract_attributes();
-// true in the dev library (make dev, -DEWH_DEV): kernel A/B modes 3-6, 8-13 compiled in
+// true in the dev library (make dev, -DEWH_DEV): kernel A/B modes 3-6, 8-15 compiled in
 bool ab_variants_built();
 
 }  // namespace ewh_dev

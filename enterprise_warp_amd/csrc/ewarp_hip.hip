@@ -1313,7 +1313,9 @@ int run_white(DevCtx* h, int p, const double* theta, int ldth, int b0, int nb) {
   hipLaunchKernelGGL(wn_weights_kernel, dim3(nb), dim3(256), 0, h->stream, ps.dev, theta, ldth, b0, h->d_w,
                      h->d_beta, h->d_Kb, h->d_fac);
   if (ps.dev.n_bgroup == 0 && h->kernel_mode != 7 && ps.nb <= CONTRACT2_NB_MAX) {
-    int rc = launch_contract2_nb(ps.nb, ps.dev, h->d_w, h->d_beta, h->d_s, h->s_stride, h->d_G, nb, h->stream);
+    // (dev library A/B: mode 15 = 4 waves per sample, mode 16 = 8)
+    const int waves = h->kernel_mode == 15 ? 4 : h->kernel_mode == 16 ? 8 : 0;
+    int rc = launch_contract2_nb(ps.nb, waves, ps.dev, h->d_w, h->d_beta, h->d_s, h->s_stride, h->d_G, nb, h->stream);
     if (rc) return rc;
     EWH_HIP(hipGetLastError());
     return 0;
@@ -2129,7 +2131,7 @@ int ewh_set_fixed_white(ewh_handle* H, const double* values) {
 }
 
 int ewh_set_kernel_mode(ewh_handle* H, int32_t mode) {
-  if (!H || mode < 0 || mode > 14) return set_err(EWH_E_INVALID, "bad handle / mode");
+  if (!H || mode < 0 || mode > 16) return set_err(EWH_E_INVALID, "bad handle / mode");
   if (mode >= 3 && mode != 7 && !ab_variants_built())
     return set_err(EWH_E_UNSUPPORTED, "kernel A/B variants are built only into the dev library (make dev)");
   for (DevCtx* h : H->ctx) {

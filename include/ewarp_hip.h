@@ -252,12 +252,14 @@ double ewh_unit_cost(const ewh_handle* h, int32_t pulsar);
  * hardware rcp estimate (the default uses one cubic correction), 11 = the
  * default plus row scales by one cubic rsq correction, 12 = the default
  * without the packed phase-3 row scales (four gathers + rsqrts per block row
- * instead of one), 13 = phase split H = 3 with every row scale packed.
+ * instead of one), 13 = phase split H = 3 with every row scale packed,
+ * 14 = ALG 8 + lookahead; 15 / 16 = the pipelined contraction with 4 / 8
+ * waves per sample (default: 8 for 144+ columns, else 4).
  * 7 = default Cholesky with the round-1 kernels elsewhere: the
  * contraction (varying white noise: separate epoch-sum kernel, unpipelined
  * tiles) instead of the pipelined one and, for a correlated common process,
  * the right-looking dense update and the LDS Gauss-Jordan M_g inverse.
- * Modes 3-6 and 8-13 exist only in the dev library (`make dev`:
+ * Modes 3-6 and 8-16 exist only in the dev library (`make dev`:
  * libewarp_hip_dev.so); the product library returns EWH_E_UNSUPPORTED. */
 int ewh_set_kernel_mode(ewh_handle* h, int32_t mode);
 
