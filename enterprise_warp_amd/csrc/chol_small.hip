@@ -38,6 +38,10 @@ int launch_chol_small(int mode, int nb, const CholJob* jobs, int B, long long u0
       case 12: launch_chol_mfma<8, 1, 2, 7>(jobs, B, u0, n, b_off, theta, ldth, units, st); return 0;  // default without the packed row scales
       case 13: launch_chol_mfma<8, 1, 2, 9>(jobs, B, u0, n, b_off, theta, ldth, units, st); return 0;  // phase split H = 3, every row scale packed
       case 14: launch_chol_mfma<8, 1, 2, 10>(jobs, B, u0, n, b_off, theta, ldth, units, st); return 0;  // ALG 8 + lookahead (trailing MFMAs inside the next panel)
+      case 17: launch_chol_mfma<8, 1, 2, 11>(jobs, B, u0, n, b_off, theta, ldth, units, st); return 0;  // ALG 8 with fused DPP multiply-adds
+      case 18: launch_chol_mfma<8, 1, 2, 12>(jobs, B, u0, n, b_off, theta, ldth, units, st); return 0;  // + replicated pivot rows (no bpermute in the chain)
+      case 20: launch_chol_mfma<8, 1, 2, 14>(jobs, B, u0, n, b_off, theta, ldth, units, st); return 0;  // ALG 11 + staggered first generation
+      case 19: launch_chol_mfma<8, 1, 2, 13>(jobs, B, u0, n, b_off, theta, ldth, units, st); return 0;  // + issue order pinned by sched barriers
       default: break;
     }
   }

@@ -620,6 +620,62 @@ __device__ __forceinline__ double row_newbcast_rows(double x) {
   return __builtin_bit_cast(double, v);
 }
 
+// One pivot k = 4 KR + KQ of the blocked panel (ALG 11) as fused DP-ALU DPP
+// multiply-adds: the row update A[q+4r][c] += A[q+4r][k] * nw (r > KR; r = KR
+// only in the 16-lane rows q > KQ, by row_mask) and, with DOE, the column
+// operation E[q+4r][c] += E[q+4r][k] * nwm (r <= KR; nwm is 0 in the lanes
+// c <= k), each ONE v_fmac_f64_dpp with src0 read from lane k of its 16-lane
+// row (row_newbcast).  The DPP-mov + fma pairs of ALG 8 compute the same
+// products and sums, so the results are bit-identical; half the VALU issue.
+// Hazards the compiler cannot see inside the asm: (1) a DPP source must be
+// written >= 2 wait states before it is read -- one statement per pivot, and
+// the next pivot's statement needs nw, whose chain (readlane of this
+// statement's output, rcp, 3 fma) lies in between; pivot 0 follows the
+// compiler's E initialisation, hence its s_nop; (2) E is an MFMA operand (V =
+// E^T A) right after the last column operation (k = 14): a trailing s_nop
+// covers VALU-write -> MFMA-read.  Only live registers (blk, E) are written,
+// so no in-flight MFMA reads them as a dead source.
+// NOP: s_nop 1 first -- pivot 0 (after the compiler's E initialisation) and
+// every pivot of ALG 12, whose statements have no dependency chain between
+// them (the chain runs through row_fmac_bcast).
+template <int K, int KR, int KQ, bool DOE, bool NOP>
+__device__ __forceinline__ void pivot_fused(v4d& A, v4d& E, double nw, double nwm) {
+  double a0 = A[0], a1 = A[1], a2 = A[2], a3 = A[3];
+  double e0 = E[0], e1 = E[1], e2 = E[2], e3 = E[3];
+  constexpr int RM = (0xf << (KQ + 1)) & 0xf;   // rows q > KQ of register KR
+  asm(".if %[nop]\n s_nop 1\n .endif\n"
+      ".if %[kr] < 1\n v_fmac_f64_dpp %[a1], %[a1], %[nw] row_newbcast:%[k] row_mask:0xf bank_mask:0xf\n .endif\n"
+      ".if %[kr] < 2\n v_fmac_f64_dpp %[a2], %[a2], %[nw] row_newbcast:%[k] row_mask:0xf bank_mask:0xf\n .endif\n"
+      ".if %[kr] < 3\n v_fmac_f64_dpp %[a3], %[a3], %[nw] row_newbcast:%[k] row_mask:0xf bank_mask:0xf\n .endif\n"
+      ".if %[rm] != 0\n"
+      " .if %[kr] == 0\n v_fmac_f64_dpp %[a0], %[a0], %[nw] row_newbcast:%[k] row_mask:%[rm] bank_mask:0xf\n .endif\n"
+      " .if %[kr] == 1\n v_fmac_f64_dpp %[a1], %[a1], %[nw] row_newbcast:%[k] row_mask:%[rm] bank_mask:0xf\n .endif\n"
+      " .if %[kr] == 2\n v_fmac_f64_dpp %[a2], %[a2], %[nw] row_newbcast:%[k] row_mask:%[rm] bank_mask:0xf\n .endif\n"
+      " .if %[kr] == 3\n v_fmac_f64_dpp %[a3], %[a3], %[nw] row_newbcast:%[k] row_mask:%[rm] bank_mask:0xf\n .endif\n"
+      ".endif\n"
+      ".if %[doe]\n"
+      " v_fmac_f64_dpp %[e0], %[e0], %[nwm] row_newbcast:%[k] row_mask:0xf bank_mask:0xf\n"
+      " .if %[kr] >= 1\n v_fmac_f64_dpp %[e1], %[e1], %[nwm] row_newbcast:%[k] row_mask:0xf bank_mask:0xf\n .endif\n"
+      " .if %[kr] >= 2\n v_fmac_f64_dpp %[e2], %[e2], %[nwm] row_newbcast:%[k] row_mask:0xf bank_mask:0xf\n .endif\n"
+      " .if %[kr] >= 3\n v_fmac_f64_dpp %[e3], %[e3], %[nwm] row_newbcast:%[k] row_mask:0xf bank_mask:0xf\n .endif\n"
+      " .if %[k] == 14\n s_nop 7\n s_nop 7\n .endif\n"
+      ".endif\n"
+      : [a0] "+v"(a0), [a1] "+v"(a1), [a2] "+v"(a2), [a3] "+v"(a3), [e0] "+v"(e0), [e1] "+v"(e1), [e2] "+v"(e2),
+        [e3] "+v"(e3)
+      : [nw] "v"(nw), [nwm] "v"(nwm), [k] "i"(K), [kr] "i"(KR), [rm] "i"(RM), [doe] "i"(DOE ? 1 : 0),
+        [nop] "i"(NOP ? 1 : 0));
+  A[0] = a0; A[1] = a1; A[2] = a2; A[3] = a3;
+  E[0] = e0; E[1] = e1; E[2] = e2; E[3] = e3;
+}
+
+// x += x[lane k of the 16-lane row] * w (one v_fmac_f64_dpp), after 2 wait
+// states: ALG 12 applies it to the replicated copies of the next two pivot
+// rows, whose sources another such statement may have written just before.
+template <int K>
+__device__ __forceinline__ void row_fmac_bcast(double& x, double w) {
+  asm("s_nop 1\n v_fmac_f64_dpp %0, %0, %1 row_newbcast:%2 row_mask:0xf bank_mask:0xf" : "+v"(x) : "v"(w), "i"(K));
+}
+
 // upper-triangle blocks (i, j), r0 <= i < r1, i <= j < NB, enumerated row by
 // row: count, and block t -> (i, j)
 constexpr int tri_count(int nb, int r0, int r1) {
@@ -685,12 +741,55 @@ __device__ __forceinline__ void panel_ldl_row(BBt BBc, Blk&& blk, int q, int c, 
       constexpr int r = decltype(R)::value;
       E[r] = (q + 4 * r == c) ? 1.0 : 0.0;
     });
+    // ALG 12: R = pivot row k, replicated over the four 16-lane row groups
+    // (R[c] = A[k][c] in every lane of column c); R1, R2 = the next two rows as
+    // they stood before this pivot.  Pivot k turns R1 into the next R and
+    // brings R2 up to date by the same fused multiply-add the block rows
+    // take; the row after them is fetched by ds_bpermute right after the
+    // block-row update and is not needed for two pivots, so the per-pivot
+    // dependency chain (R -> d, 1/d -> nw -> R1) has no LDS round trip.
+    constexpr int NPIV = (RL && bb == NB - 1) ? 15 : 16;
+    // ALG 13: the same with the issue order pinned by scheduling barriers:
+    // nw, then R1 and the next pivot's readlane, then the rest of the pivot.
+    constexpr bool RP = ALG == 12 || ALG == 13;
+    double R = 0.0, R1 = 0.0, R2 = 0.0, dn = 0.0;
+    if constexpr (RP) {
+      R = __shfl(blk(BBc)[0], c);
+      R1 = __shfl(blk(BBc)[0], 16 + c);
+      R2 = __shfl(blk(BBc)[0], 32 + c);
+      dn = readlane_d(R, 0);
+    }
     static_for<0, 4>([&](auto KR) {
       constexpr int kr = decltype(KR)::value;
       constexpr int nk = (RL && bb == NB - 1 && kr == 3) ? 3 : 4;   // the r column is not pivoted
       static_for<0, nk>([&](auto KQc) {
         constexpr int kq = decltype(KQc)::value;
         constexpr int k = 4 * kr + kq;
+        if constexpr (ALG >= 11 && ALG <= 13) {
+          // fused DPP multiply-adds (pivot_fused): nw = -A[k][c] / d_k, the
+          // column operations take it only in the lanes c > k
+          constexpr bool doe = (bb < NB - 1 || !RL) && k < 15;
+          constexpr bool nxt = RP && k + 1 < NPIV;
+          const double xk = RP ? R : __shfl(blk(BBc)[kr], 16 * kq + c);
+          const double d = RP ? dn : readlane_d(blk(BBc)[kr], 16 * kq + k);
+          const double nw = div_fast(-xk, d);
+          if constexpr (nxt) {
+            row_fmac_bcast<k>(R1, nw);
+            dn = readlane_d(R1, k + 1);
+          }
+          if constexpr (ALG == 13) __builtin_amdgcn_sched_barrier(0);
+          const double nwm = (doe && c > k) ? nw : 0.0;
+          if constexpr (RP && k + 2 < NPIV) row_fmac_bcast<k>(R2, nw);
+          pivot_fused<k, kr, kq, doe, (k == 0 || RP)>(blk(BBc), E, nw, nwm);
+          if constexpr (nxt) {
+            R = R1;
+            R1 = R2;
+            if constexpr (k + 3 < NPIV) R2 = __shfl(blk(BBc)[(k + 3) / 4], 16 * ((k + 3) % 4) + c);
+          }
+          if constexpr (ALG == 13) __builtin_amdgcn_sched_barrier(0);
+          fill(std::integral_constant<int, k>{});
+          return;
+        }
         const double d = readlane_d(blk(BBc)[kr], 16 * kq + k);
         // raw multipliers A[q + 4r][k] (rows > k): register kr only in the
         // 16-lane rows q > kq (DPP row_mask; disabled rows read 0)
@@ -842,7 +941,7 @@ __device__ __forceinline__ void panel_ldl_row(BBt BBc, Blk&& blk, int q, int c, 
   // rows of the block row -> U = d^-1/2 V, d of row q + 4r read from the
   // diagonal (lane 17q + 4r); log-det and positivity from one lane per row
   // (c == 0); the r row (last block, row 15) is left as it is
-  if constexpr (((ALG == 8 || ALG == 10) && bb >= Split<NB, ALG>::H) || ALG == 9) {
+  if constexpr (((ALG == 8 || ALG >= 10) && bb >= Split<NB, ALG>::H) || ALG == 9) {
     // (phase 3 only: in phase 1 the extra temporaries spill)
     // packed: lane (q, c) takes d of row q + 4 (c/4) -- held in register c/4
     // of lane (q, q + 4 (c/4)), whose own c/4 is the same -- so one gather,
@@ -881,11 +980,21 @@ __device__ __forceinline__ void panel_ldl_row(BBt BBc, Blk&& blk, int q, int c, 
 // (pulsar-major: a device's pulsar range is one contiguous slice, the unit an
 // all-gather moves), and
 // the unit term is the local part K - 1/2 log|Sigma_LL| - 1/2 log|phi_L|.
-template <int NB, int FULL, int W, int ALG = 0, int KEEP = 0>
+// ALG0 14 (A/B): ALG 11 with the first generation of units started at
+// scattered times (0-3k cycles), so the two units sharing a SIMD do not run
+// their latency-bound panels in lockstep.
+template <int NB, int FULL, int W, int ALG0 = 0, int KEEP = 0>
 __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(W, W)))
 void chol_mfma_kernel(const CholJob* __restrict__ jobs, int B, long long u0, int b_off,
                       const double* __restrict__ theta, int ldth, double* __restrict__ out_units,
                       double* __restrict__ keep_out, int keep_b0, int keep_bs) {
+  constexpr int ALG = ALG0 == 14 ? 11 : ALG0;
+  if constexpr (ALG0 == 14) {
+    if (blockIdx.x < 2048) {
+      const unsigned n = (blockIdx.x * 2654435761u >> 26) % 48u;
+      for (unsigned i = 0; i < n; ++i) __builtin_amdgcn_s_sleep(1);
+    }
+  }
   constexpr int LD = 16 * NB;
   using S = Split<NB, ALG>;
   constexpr int H = S::H;
