@@ -728,6 +728,10 @@ __device__ __forceinline__ void panel_ldl_row(BBt BBc, Blk&& blk, int q, int c, 
   constexpr int bb = decltype(BBc)::value;
   static_assert(ALG < 3 || FULL, "the DPP panel needs compile-time pivots");
   if constexpr (ALG >= 5) {
+    // ALG 16/17: the pivots run at raised wave priority, so their dependent
+    // VALU chain is not starved by the partner wave's back-to-back MFMAs
+    constexpr bool PRIO = ALG == 16 || ALG == 17;
+    if constexpr (PRIO) __builtin_amdgcn_s_setprio(2);
     // ALG 5 (blocked panel): eliminate the 16x16 diagonal block alone (rows >
     // k take row k, u_i from its symmetric lower part by DPP as ALG 3/4)
     // while E = L^-T accumulates the matching COLUMN operations
@@ -765,7 +769,7 @@ __device__ __forceinline__ void panel_ldl_row(BBt BBc, Blk&& blk, int q, int c, 
       static_for<0, nk>([&](auto KQc) {
         constexpr int kq = decltype(KQc)::value;
         constexpr int k = 4 * kr + kq;
-        if constexpr (ALG >= 11 && ALG <= 13) {
+        if constexpr ((ALG >= 11 && ALG <= 13) || ALG == 16 || ALG == 17) {
           // fused DPP multiply-adds (pivot_fused): nw = -A[k][c] / d_k, the
           // column operations take it only in the lanes c > k
           constexpr bool doe = (bb < NB - 1 || !RL) && k < 15;
@@ -819,6 +823,7 @@ __device__ __forceinline__ void panel_ldl_row(BBt BBc, Blk&& blk, int q, int c, 
         fill(std::integral_constant<int, k>{});
       });
     });
+    if constexpr (PRIO) __builtin_amdgcn_s_setprio(0);
     if constexpr (bb < NB - 1 || !RL) fill.on_e(E);
     static_for<bb + 1, NB>([&](auto JJ) {
       v4d acc = {0.0, 0.0, 0.0, 0.0};
@@ -980,6 +985,13 @@ __device__ __forceinline__ void panel_ldl_row(BBt BBc, Blk&& blk, int q, int c, 
 // (pulsar-major: a device's pulsar range is one contiguous slice, the unit an
 // all-gather moves), and
 // the unit term is the local part K - 1/2 log|Sigma_LL| - 1/2 log|phi_L|.
+#ifdef EWH_DEV
+// ALG0 15 (dev diagnostics): ALG 11 with s_memtime stamps at the phase
+// boundaries of the units with blockIdx < STAMP_UNITS (ewh_dev_stamps)
+constexpr int STAMP_UNITS = 4096, STAMP_N = 24;
+static __device__ long long g_stamps[STAMP_UNITS * STAMP_N];
+#endif
+
 // ALG0 14 (A/B): ALG 11 with the first generation of units started at
 // scattered times (0-3k cycles), so the two units sharing a SIMD do not run
 // their latency-bound panels in lockstep.
@@ -988,7 +1000,20 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(W, W)))
 void chol_mfma_kernel(const CholJob* __restrict__ jobs, int B, long long u0, int b_off,
                       const double* __restrict__ theta, int ldth, double* __restrict__ out_units,
                       double* __restrict__ keep_out, int keep_b0, int keep_bs) {
-  constexpr int ALG = ALG0 == 14 ? 11 : ALG0;
+  constexpr int ALG = (ALG0 == 14 || ALG0 == 15 || ALG0 == 18 || ALG0 == 19) ? 11 : ALG0;
+  long long stp[24];
+#ifdef EWH_DEV
+#define EWH_STAMP(I)                                            \
+  if constexpr (ALG0 == 15) {                                   \
+    __builtin_amdgcn_sched_barrier(0);                          \
+    stp[(I)] = (long long)__builtin_amdgcn_s_memtime();         \
+    __builtin_amdgcn_sched_barrier(0);                          \
+  }
+#else
+#define EWH_STAMP(I)
+#endif
+  EWH_STAMP(0)
+  if constexpr (ALG0 == 17) __builtin_amdgcn_s_setprio(2);
   if constexpr (ALG0 == 14) {
     if (blockIdx.x < 2048) {
       const unsigned n = (blockIdx.x * 2654435761u >> 26) % 48u;
@@ -1009,12 +1034,28 @@ void chol_mfma_kernel(const CholJob* __restrict__ jobs, int B, long long u0, int
   const double* A = J.mats + (long long)(b - b_off) * J.mstride;
   const double* th = theta + (long long)b * ldth;
 
+  // ALG0 18: block row 0 of the matrix is loaded before the spectra are
+  // formed, so its latency overlaps the prologue (phinv is added after)
+  constexpr bool PRE = ALG0 == 18;
+  v4d pre[PRE ? NB : 1];
+  if constexpr (PRE) {
+    static_for<0, NB>([&](auto BJ) {
+      static_for<0, 4>([&](auto R) {
+        constexpr int r = decltype(R)::value;
+        pre[decltype(BJ)::value][r] = A[(long long)(q + 4 * r) * LD + 16 * decltype(BJ)::value + c];
+      });
+    });
+  }
   LogAcc lphi;
   for (int a = lane; a < LD; a += 64) {
     double pi = 0.0;
     if (a < J.mreal && J.col_ptr[a] < J.col_ptr[a + 1]) {   // (pads carry no entry)
       double ph = 0.0;
-      for (int e = J.col_ptr[a]; e < J.col_ptr[a + 1]; ++e) ph += spec_phi_body(J.spec[e], th);
+      if constexpr (ALG0 == 19) {
+        ph = 1.0 + 1e-3 * a;   // diagnostic: no spectra (wrong values)
+      } else {
+        for (int e = J.col_ptr[a]; e < J.col_ptr[a + 1]; ++e) ph += spec_phi_body(J.spec[e], th);
+      }
       pi = 1.0 / ph;
       lphi.add(ph);
     }
@@ -1026,6 +1067,8 @@ void chol_mfma_kernel(const CholJob* __restrict__ jobs, int B, long long u0, int
   // factorisation: spilled to scratch and reloaded serially at the end)
   const double lphi_sum = ALG >= 1 ? 0.0 : wave_sum(lphi.value());
   __syncthreads();
+  EWH_STAMP(1)
+  if constexpr (ALG0 == 17) __builtin_amdgcn_s_setprio(0);
 
   auto load_block = [&](auto BI, auto BJ, v4d& v) {
     constexpr int bi = decltype(BI)::value, bj = decltype(BJ)::value;
@@ -1103,7 +1146,21 @@ void chol_mfma_kernel(const CholJob* __restrict__ jobs, int B, long long u0, int
   v4d U1[S::n1 > 0 ? S::n1 : 1];
   static_for<0, H>([&](auto BI) {
     constexpr int bi = decltype(BI)::value;
-    static_for<bi, NB>([&](auto BJ) { load_block(BI, BJ, U1[S::i1(bi, decltype(BJ)::value)]); });
+    static_for<bi, NB>([&](auto BJ) {
+      constexpr int bj = decltype(BJ)::value;
+      if constexpr (PRE && bi == 0) {
+        U1[S::i1(0, bj)] = pre[bj];
+        if constexpr (bj == 0) {
+          const double pd = phinv[c];
+          static_for<0, 4>([&](auto R) {
+            constexpr int r = decltype(R)::value;
+            U1[S::i1(0, 0)][r] += (q + 4 * r == c) ? pd : 0.0;
+          });
+        }
+      } else {
+        load_block(BI, BJ, U1[S::i1(bi, bj)]);
+      }
+    });
   });
   // ALG 10 (lookahead): step bb updates only the next row (bb + 1) at once; its
   // updates of rows >= bb + 2 are spread over the pivots of panel bb + 1
@@ -1124,6 +1181,7 @@ void chol_mfma_kernel(const CholJob* __restrict__ jobs, int B, long long u0, int
       }
     };
     panel(BBc, [&](auto JJ) -> v4d& { return U1[S::i1(bb, decltype(JJ)::value)]; }, fill);
+    EWH_STAMP(2 + 2 * bb)
     static_for<bb + 1, (LA ? (bb + 2 < H ? bb + 2 : H) : H)>([&](auto II) {
       constexpr int i = decltype(II)::value;
       static_for<i, NB>([&](auto JJ) {
@@ -1131,6 +1189,7 @@ void chol_mfma_kernel(const CholJob* __restrict__ jobs, int B, long long u0, int
         syrk_update(U1[S::i1(i, j)], U1[S::i1(bb, i)], U1[S::i1(bb, j)]);
       });
     });
+    EWH_STAMP(3 + 2 * bb)
   });
   // ---- phase 2: A22 -= U12^T U12 ----
   // block by block in row order: U1 column i is dead once row i of A22 is done
@@ -1146,6 +1205,7 @@ void chol_mfma_kernel(const CholJob* __restrict__ jobs, int B, long long u0, int
       });
     });
   });
+  EWH_STAMP(2 + 2 * H)
   // ---- phase 3: factor A22 (up to the kept blocks) ----
   static_for<H, NB - KEEP>([&](auto BBc) {
     constexpr int bb = decltype(BBc)::value;
@@ -1162,6 +1222,7 @@ void chol_mfma_kernel(const CholJob* __restrict__ jobs, int B, long long u0, int
       }
     };
     panel(BBc, [&](auto JJ) -> v4d& { return U2[S::i2(bb, decltype(JJ)::value)]; }, fill);
+    EWH_STAMP(3 + 2 * bb)
     constexpr bool last = bb == NB - KEEP - 1;
     static_for<bb + 1, ((LA && !last) ? (bb + 2 < NB ? bb + 2 : NB) : NB)>([&](auto II) {
       constexpr int i = decltype(II)::value;
@@ -1170,6 +1231,7 @@ void chol_mfma_kernel(const CholJob* __restrict__ jobs, int B, long long u0, int
         syrk_update(U2[S::i2(i, j)], U2[S::i2(bb, i)], U2[S::i2(bb, j)]);
       });
     });
+    EWH_STAMP(4 + 2 * bb)
   });
   double qv = 0.0;
   if constexpr (KEEP == 0) {
@@ -1204,6 +1266,18 @@ void chol_mfma_kernel(const CholJob* __restrict__ jobs, int B, long long u0, int
     if (!ok_all || J.fail) lnl = -INFINITY;
     out_units[(long long)p * B + b] = lnl;
   }
+#ifdef EWH_DEV
+  if constexpr (ALG0 == 15) {
+    EWH_STAMP(3 + 2 * NB)
+    if (lane == 0 && blockIdx.x < STAMP_UNITS) {
+      long long* o = g_stamps + (long long)blockIdx.x * STAMP_N;
+      for (int i = 0; i < 4 + 2 * NB && i < STAMP_N - 2; ++i) o[i] = stp[i];
+      o[STAMP_N - 2] = __builtin_amdgcn_s_getreg(4 | (31 << 11));    // HW_ID (wave, SIMD, CU, SE)
+      o[STAMP_N - 1] = __builtin_amdgcn_s_getreg(20 | (31 << 11));   // XCC_ID
+    }
+  }
+#endif
+#undef EWH_STAMP
 }
 
 // ----------------------------------------------------------------------------

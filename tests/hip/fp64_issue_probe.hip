@@ -15,13 +15,14 @@ constexpr int ITERS = 256;
 
 enum Op {
   NONE, MFMA, MFMA1, MFMA2, MFMA8, FMA_IND, FMA_DEP, FMACDPP_IND, FMACDPP_DEP, MOVDPP_IND, RLANE_IND, BPERM_IND, BPERM_DEP,
-  RCP_IND, RCP_DEP, CND_IND, NOP0, MUL_IND, FMAC_IND, NOP1
+  RCP_IND, RCP_DEP, CND_IND, NOP0, MUL_IND, FMAC_IND, NOP1, MFMA_ASM4, MFMA_ASM8
 };
 static const char* NAMES[] = {"none", "mfma_f64_16x16x4 x4 chains", "mfma x1 chain", "mfma x2 chains", "mfma x8 chains", "v_fma_f64 indep", "v_fma_f64 dep chain",
                               "v_fmac_f64_dpp indep", "v_fmac_f64_dpp+s_nop1 dep", "v_mov_b64_dpp indep",
                               "v_readlane_b32 indep", "ds_bpermute_b32 indep", "ds_bpermute+wait dep",
                               "v_rcp_f64 indep", "v_rcp_f64 dep chain", "v_cndmask_b32 indep", "s_nop 0",
-                              "v_mul_f64 indep", "v_fmac_f64_e32 indep", "s_nop 1"};
+                              "v_mul_f64 indep", "v_fmac_f64_e32 indep", "s_nop 1",
+                              "asm mfma x4 acc (16/blk)", "asm mfma x8 acc (16/blk)"};
 
 #define R16(x) x x x x x x x x x x x x x x x x
 
@@ -97,6 +98,24 @@ __device__ __forceinline__ void body(double* v, double w) {
     asm volatile(R16("v_fmac_f64_e32 %0, %8, %8\n v_fmac_f64_e32 %1, %8, %8\n v_fmac_f64_e32 %2, %8, %8\n v_fmac_f64_e32 %3, %8, %8\n"
                      "v_fmac_f64_e32 %4, %8, %8\n v_fmac_f64_e32 %5, %8, %8\n v_fmac_f64_e32 %6, %8, %8\n v_fmac_f64_e32 %7, %8, %8\n")
                  : "+v"(v[0]), "+v"(v[1]), "+v"(v[2]), "+v"(v[3]), "+v"(v[4]), "+v"(v[5]), "+v"(v[6]), "+v"(v[7]) : "v"(w));
+  } else if constexpr (OP == MFMA_ASM4 || OP == MFMA_ASM8) {
+    // 16 MFMAs round-robin over 4 or 8 accumulators held across calls (no
+    // per-call setup); pure issue / pipe throughput
+    typedef double v4d __attribute__((ext_vector_type(4)));
+    static_assert(sizeof(v4d) == 32, "");
+    v4d* acc = reinterpret_cast<v4d*>(v);   // v has room for 8 v4d (see k_pair)
+    if constexpr (OP == MFMA_ASM4) {
+      asm volatile(R16("v_mfma_f64_16x16x4_f64 %0, %4, %5, %0\n" "v_mfma_f64_16x16x4_f64 %1, %4, %5, %1\n"
+                       "v_mfma_f64_16x16x4_f64 %2, %4, %5, %2\n" "v_mfma_f64_16x16x4_f64 %3, %4, %5, %3\n")
+                   : "+v"(acc[0]), "+v"(acc[1]), "+v"(acc[2]), "+v"(acc[3]) : "v"(w), "v"(v[32]));
+    } else {
+      asm volatile(R16("v_mfma_f64_16x16x4_f64 %0, %8, %9, %0\n" "v_mfma_f64_16x16x4_f64 %1, %8, %9, %1\n"
+                       "v_mfma_f64_16x16x4_f64 %2, %8, %9, %2\n" "v_mfma_f64_16x16x4_f64 %3, %8, %9, %3\n"
+                       "v_mfma_f64_16x16x4_f64 %4, %8, %9, %4\n" "v_mfma_f64_16x16x4_f64 %5, %8, %9, %5\n"
+                       "v_mfma_f64_16x16x4_f64 %6, %8, %9, %6\n" "v_mfma_f64_16x16x4_f64 %7, %8, %9, %7\n")
+                   : "+v"(acc[0]), "+v"(acc[1]), "+v"(acc[2]), "+v"(acc[3]), "+v"(acc[4]), "+v"(acc[5]), "+v"(acc[6]),
+                     "+v"(acc[7]) : "v"(w), "v"(v[32]));
+    }
   } else if constexpr (OP == NOP1) {
     asm volatile(R16("s_nop 1\n s_nop 1\n s_nop 1\n s_nop 1\n s_nop 1\n s_nop 1\n s_nop 1\n s_nop 1\n") ::);
   }
@@ -104,15 +123,15 @@ __device__ __forceinline__ void body(double* v, double w) {
 
 // instructions per body() call
 constexpr int per_call(int op) {
-  return op == MFMA || op == MFMA1 || op == MFMA2 || op == MFMA8 ? 16 : op == FMA_DEP || op == FMACDPP_DEP || op == RCP_DEP || op == BPERM_DEP ? 16
+  return op == MFMA_ASM4 ? 64 : op == MFMA_ASM8 ? 128 : op == MFMA || op == MFMA1 || op == MFMA2 || op == MFMA8 ? 16 : op == FMA_DEP || op == FMACDPP_DEP || op == RCP_DEP || op == BPERM_DEP ? 16
        : op == RLANE_IND || op == CND_IND ? 64 : 128;
 }
 
 template <int OA, int OB>
 __global__ __launch_bounds__(512) void k_pair(double seed, double* sink, long long* cyc) {
   const int wave = threadIdx.x >> 6;
-  double v[8];
-  for (int j = 0; j < 8; ++j) v[j] = seed + j * 1e-3 + threadIdx.x * 1e-6;
+  double v[40];
+  for (int j = 0; j < 40; ++j) v[j] = seed + j * 1e-3 + threadIdx.x * 1e-6;
   const double w = 0.999 + threadIdx.x * 1e-9;
   __syncthreads();
   const long long t0 = (long long)__builtin_amdgcn_s_memtime();
@@ -123,7 +142,7 @@ __global__ __launch_bounds__(512) void k_pair(double seed, double* sink, long lo
   }
   const long long t1 = (long long)__builtin_amdgcn_s_memtime();
   double s = 0;
-  for (int j = 0; j < 8; ++j) s += v[j];
+  for (int j = 0; j < 40; ++j) s += v[j];
   sink[blockIdx.x * 512 + threadIdx.x] = s;
   if ((threadIdx.x & 63) == 0) cyc[blockIdx.x * 8 + wave] = t1 - t0;
 }
@@ -155,6 +174,15 @@ int main() {
   long long* cyc;
   (void)hipMalloc(&sink, 256 * 512 * sizeof(double));
   (void)hipMalloc(&cyc, 256 * 8 * sizeof(long long));
+  run<MFMA_ASM4, NONE>(sink, cyc);
+  run<MFMA_ASM8, NONE>(sink, cyc);
+  run<MFMA_ASM4, MFMA_ASM4>(sink, cyc);
+  run<MFMA_ASM8, MFMA_ASM8>(sink, cyc);
+  run<MFMA_ASM8, FMA_IND>(sink, cyc);
+  run<MFMA_ASM8, FMA_DEP>(sink, cyc);
+  run<MFMA_ASM8, FMACDPP_IND>(sink, cyc);
+  run<MFMA_ASM8, BPERM_DEP>(sink, cyc);
+  run<MFMA_ASM8, RCP_DEP>(sink, cyc);
   run<MFMA1, NONE>(sink, cyc);
   run<MFMA2, NONE>(sink, cyc);
   run<MFMA, NONE>(sink, cyc);
