@@ -51,6 +51,8 @@ int launch_chol_small(int mode, int nb, const CholJob* jobs, int B, long long u0
       case 23: launch_chol_mfma<8, 1, 2, 17>(jobs, B, u0, n, b_off, theta, ldth, units, st); return 0;  // + in the phi prologue
       case 24: launch_chol_mfma<8, 1, 2, 11>(jobs, B, u0, n, b_off, theta, ldth, units, st); return 0;  // ALG 11 without the early block-row-0 load
       case 25: launch_chol_mfma<8, 1, 2, 19>(jobs, B, u0, n, b_off, theta, ldth, units, st); return 0;  // diagnostic: no spectra (wrong values)
+      case 26: launch_chol_mfma<8, 1, 2, 20>(jobs, B, u0, n, b_off, theta, ldth, units, st); return 0;  // default (ALG0 18) + phase stamps
+      case 27: launch_chol_mfma<8, 1, 2, 21>(jobs, B, u0, n, b_off, theta, ldth, units, st); return 0;  // default + A22 blocks loaded during phase 1
       case 21: launch_chol_mfma<8, 1, 2, 15>(jobs, B, u0, n, b_off, theta, ldth, units, st); return 0;  // ALG 11 + phase stamps
       case 20: launch_chol_mfma<8, 1, 2, 14>(jobs, B, u0, n, b_off, theta, ldth, units, st); return 0;  // ALG 11 + staggered first generation
       case 19: launch_chol_mfma<8, 1, 2, 13>(jobs, B, u0, n, b_off, theta, ldth, units, st); return 0;  // + issue order pinned by sched barriers

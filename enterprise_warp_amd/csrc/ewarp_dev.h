@@ -1000,11 +1000,11 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(W, W)))
 void chol_mfma_kernel(const CholJob* __restrict__ jobs, int B, long long u0, int b_off,
                       const double* __restrict__ theta, int ldth, double* __restrict__ out_units,
                       double* __restrict__ keep_out, int keep_b0, int keep_bs) {
-  constexpr int ALG = (ALG0 == 14 || ALG0 == 15 || ALG0 == 18 || ALG0 == 19) ? 11 : ALG0;
+  constexpr int ALG = (ALG0 == 14 || ALG0 == 15 || (ALG0 >= 18 && ALG0 <= 21)) ? 11 : ALG0;
   long long stp[24];
 #ifdef EWH_DEV
 #define EWH_STAMP(I)                                            \
-  if constexpr (ALG0 == 15) {                                   \
+  if constexpr (ALG0 == 15 || ALG0 == 20) {                     \
     __builtin_amdgcn_sched_barrier(0);                          \
     stp[(I)] = (long long)__builtin_amdgcn_s_memtime();         \
     __builtin_amdgcn_sched_barrier(0);                          \
@@ -1036,7 +1036,7 @@ void chol_mfma_kernel(const CholJob* __restrict__ jobs, int B, long long u0, int
 
   // ALG0 18: block row 0 of the matrix is loaded before the spectra are
   // formed, so its latency overlaps the prologue (phinv is added after)
-  constexpr bool PRE = ALG0 == 18;
+  constexpr bool PRE = ALG0 == 18 || ALG0 == 20 || ALG0 == 21;
   v4d pre[PRE ? NB : 1];
   if constexpr (PRE) {
     static_for<0, NB>([&](auto BJ) {
@@ -1144,6 +1144,12 @@ void chol_mfma_kernel(const CholJob* __restrict__ jobs, int B, long long u0, int
 
   // ---- phase 1: block rows 0..H-1 ----
   v4d U1[S::n1 > 0 ? S::n1 : 1];
+  // ALG0 21: the A22 blocks phase 2 starts from are loaded during phase 1, a
+  // few after each trailing update -- as many as that update retired (the
+  // blocks (bb, j < H) are dead once rows < H are updated)
+  constexpr bool EA = ALG0 == 21 && S::n2 > 0;
+  v4d A22[EA ? S::n2 : 1];
+  auto ea_count = [](int bb) { return (bb + 1) * H - bb * (bb + 1) / 2; };   // blocks retired by row bb
   static_for<0, H>([&](auto BI) {
     constexpr int bi = decltype(BI)::value;
     static_for<bi, NB>([&](auto BJ) {
@@ -1190,7 +1196,19 @@ void chol_mfma_kernel(const CholJob* __restrict__ jobs, int B, long long u0, int
       });
     });
     EWH_STAMP(3 + 2 * bb)
+    if constexpr (EA) {
+      constexpr int t0 = bb == 0 ? 0 : ((bb * H - (bb - 1) * bb / 2) < S::n2 ? (bb * H - (bb - 1) * bb / 2) : S::n2);
+      constexpr int t1 = ((bb + 1) * H - bb * (bb + 1) / 2) < S::n2 ? ((bb + 1) * H - bb * (bb + 1) / 2) : S::n2;
+      static_for<t0, (bb == H - 1 ? S::n2 : t1)>([&](auto T) {
+        constexpr int i = tri_row(NB, H, decltype(T)::value), j = tri_col(NB, H, decltype(T)::value);
+        static_for<0, 4>([&](auto R) {
+          constexpr int r = decltype(R)::value;
+          A22[decltype(T)::value][r] = A[(long long)(16 * i + q + 4 * r) * LD + 16 * j + c];
+        });
+      });
+    }
   });
+  (void)ea_count;
   // ---- phase 2: A22 -= U12^T U12 ----
   // block by block in row order: U1 column i is dead once row i of A22 is done
   v4d U2[S::n2];
@@ -1198,7 +1216,18 @@ void chol_mfma_kernel(const CholJob* __restrict__ jobs, int B, long long u0, int
     constexpr int i = decltype(II)::value;
     static_for<i, NB>([&](auto JJ) {
       constexpr int j = decltype(JJ)::value;
-      load_block(II, JJ, U2[S::i2(i, j)]);
+      if constexpr (EA) {
+        U2[S::i2(i, j)] = A22[S::i2(i, j)];
+        if constexpr (i == j) {
+          const double pd = phinv[16 * i + c];
+          static_for<0, 4>([&](auto R) {
+            constexpr int r = decltype(R)::value;
+            U2[S::i2(i, j)][r] += (q + 4 * r == c) ? pd : 0.0;
+          });
+        }
+      } else {
+        load_block(II, JJ, U2[S::i2(i, j)]);
+      }
       static_for<0, H>([&](auto BBc) {
         constexpr int bb = decltype(BBc)::value;
         syrk_update(U2[S::i2(i, j)], U1[S::i1(bb, i)], U1[S::i1(bb, j)]);
@@ -1267,7 +1296,7 @@ void chol_mfma_kernel(const CholJob* __restrict__ jobs, int B, long long u0, int
     out_units[(long long)p * B + b] = lnl;
   }
 #ifdef EWH_DEV
-  if constexpr (ALG0 == 15) {
+  if constexpr (ALG0 == 15 || ALG0 == 20) {
     EWH_STAMP(3 + 2 * NB)
     if (lane == 0 && blockIdx.x < STAMP_UNITS) {
       long long* o = g_stamps + (long long)blockIdx.x * STAMP_N;

@@ -26,7 +26,7 @@ UNITS, NST = 4096, 24
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--B", type=int, default=4096)
-    ap.add_argument("--mode", type=int, default=21)
+    ap.add_argument("--mode", type=int, default=26)
     args = ap.parse_args()
     import torch
     from enterprise_warp_amd import _lib, synth

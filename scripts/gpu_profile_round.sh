@@ -24,7 +24,7 @@ pmc() {  # pmc <name> <script args> -- counters...
   run pmc_$name 180 rocprofv3 --pmc "$@" --kernel-trace -d gpurun_out/pmc_${TAG}_$name -o run --output-format csv -- python $sargs
 }
 run bench 400 python bench.py --steps 20 --warmup 3 --cpu-seconds 10
-run rocprof 300 rocprofv3 --kernel-trace --stats -d gpurun_out/prof_$TAG -o run --output-format csv -- python bench.py --steps 20 --warmup 3 --no-cpu-baseline
+run rocprof 300 rocprofv3 --kernel-trace --stats -d gpurun_out/prof_$TAG -o run --output-format csv -- python bench.py --steps 20 --warmup 3 --no-cpu-baseline --no-latency
 run configs 400 rocprofv3 --kernel-trace --stats -d gpurun_out/profcfg_$TAG -o run --output-format csv -- python scripts/bench_configs.py --configs c2,c3,c4 --reps 3 --check 3
 CH="scripts/chol_ab.py --rounds 2 --modes 0"
 pmc sq1 "$CH" SQ_WAVE_CYCLES SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_ACTIVE_INST_ANY SQ_INSTS_VALU SQ_INSTS_MFMA SQ_INSTS_LDS SQ_INSTS_SALU
