@@ -224,6 +224,12 @@ struct CholJob {
   const double* K;           // additive constant, K[(b - b_off) * kstride]
   int kstride;
   int fail;                  // 1: lead block not positive definite -> -inf
+  // fixed white noise: columns sharing one spectrum (the sin / cos pair of a
+  // frequency) -- rep[a] = the first column with the same entries, ulist =
+  // the nu representatives; the prologue then forms each spectrum once
+  const int* rep = nullptr;
+  const int* ulist = nullptr;
+  int nu = 0;
 };
 
 // ----------------------------------------------------------------------------
@@ -721,7 +727,7 @@ struct FillOnly : NoFill {
 // cross-pulsar factorisation's diagonal blocks).
 template <int NB, int FULL, int ALG, bool RL = true, typename BBt, typename Blk, typename Fill = NoFill>
 __device__ __forceinline__ void panel_ldl_row(BBt BBc, Blk&& blk, int q, int c, LogAcc& ldet, bool& ok,
-                                              double* rowbuf, Fill&& fill = Fill{}) {
+                                              double* rowbuf, Fill&& fill = Fill{}, int klim = 16) {
   constexpr int LD = 16 * NB;
   (void)rowbuf;
   (void)LD;
@@ -770,6 +776,15 @@ __device__ __forceinline__ void panel_ldl_row(BBt BBc, Blk&& blk, int q, int c, 
         constexpr int kq = decltype(KQc)::value;
         constexpr int k = 4 * kr + kq;
         if constexpr ((ALG >= 11 && ALG <= 13) || ALG == 16 || ALG == 17) {
+          // the last panel's pad columns (k >= klim, wave-uniform: identity rows
+          // and columns, pivot 1, every multiplier 0) are no-ops: skipped, and
+          // the result is bit-identical
+          if constexpr (ALG == 11 && RL && bb == NB - 1) {
+            if (k >= klim) {
+              fill(std::integral_constant<int, k>{});
+              return;
+            }
+          }
           // fused DPP multiply-adds (pivot_fused): nw = -A[k][c] / d_k, the
           // column operations take it only in the lanes c > k
           constexpr bool doe = (bb < NB - 1 || !RL) && k < 15;
@@ -1000,7 +1015,7 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(W, W)))
 void chol_mfma_kernel(const CholJob* __restrict__ jobs, int B, long long u0, int b_off,
                       const double* __restrict__ theta, int ldth, double* __restrict__ out_units,
                       double* __restrict__ keep_out, int keep_b0, int keep_bs) {
-  constexpr int ALG = (ALG0 == 14 || ALG0 == 15 || (ALG0 >= 18 && ALG0 <= 21)) ? 11 : ALG0;
+  constexpr int ALG = (ALG0 == 14 || ALG0 == 15 || (ALG0 >= 18 && ALG0 <= 23)) ? 11 : ALG0;
   long long stp[24];
 #ifdef EWH_DEV
 #define EWH_STAMP(I)                                            \
@@ -1036,7 +1051,7 @@ void chol_mfma_kernel(const CholJob* __restrict__ jobs, int B, long long u0, int
 
   // ALG0 18: block row 0 of the matrix is loaded before the spectra are
   // formed, so its latency overlaps the prologue (phinv is added after)
-  constexpr bool PRE = ALG0 == 18 || ALG0 == 20 || ALG0 == 21;
+  constexpr bool PRE = ALG0 == 18 || ALG0 >= 20;
   v4d pre[PRE ? NB : 1];
   if constexpr (PRE) {
     static_for<0, NB>([&](auto BJ) {
@@ -1046,6 +1061,23 @@ void chol_mfma_kernel(const CholJob* __restrict__ jobs, int B, long long u0, int
       });
     });
   }
+  // ALG0 23: each distinct spectrum formed once (J.rep / J.ulist), shared
+  // through LDS; every column then takes the same value in the same lane
+  // order as before (bit-identical)
+  constexpr bool DEDUP = ALG0 == 23;
+  __shared__ double phs[DEDUP ? LD : 1];
+  const bool dedup = DEDUP && J.rep != nullptr;
+  if constexpr (DEDUP) {
+    if (dedup) {
+      for (int i = lane; i < J.nu; i += 64) {
+        const int a = J.ulist[i];
+        double ph = 0.0;
+        for (int e = J.col_ptr[a]; e < J.col_ptr[a + 1]; ++e) ph += spec_phi_body(J.spec[e], th);
+        phs[a] = ph;
+      }
+      __syncthreads();
+    }
+  }
   LogAcc lphi;
   for (int a = lane; a < LD; a += 64) {
     double pi = 0.0;
@@ -1053,6 +1085,8 @@ void chol_mfma_kernel(const CholJob* __restrict__ jobs, int B, long long u0, int
       double ph = 0.0;
       if constexpr (ALG0 == 19) {
         ph = 1.0 + 1e-3 * a;   // diagnostic: no spectra (wrong values)
+      } else if (dedup) {
+        ph = phs[J.rep[a]];
       } else {
         for (int e = J.col_ptr[a]; e < J.col_ptr[a + 1]; ++e) ph += spec_phi_body(J.spec[e], th);
       }
@@ -1089,8 +1123,12 @@ void chol_mfma_kernel(const CholJob* __restrict__ jobs, int B, long long u0, int
   if constexpr (ALG >= 1) ldet = lphi;
   bool ok = true;
   // LDL^T panel row bb (ALG >= 1)
+  // ALG0 22: skip the pad pivots of the last panel (J.mreal .. ld - 2)
+  constexpr bool SKIPPAD = (ALG0 == 22 || ALG0 == 23) && KEEP == 0;
+  const int klast = __builtin_amdgcn_readfirstlane(J.mreal - 16 * (NB - 1));
   auto panel_ldl = [&](auto BBc, auto&& blk, auto&& fill) {
-    panel_ldl_row<NB, FULL, ALG>(BBc, blk, q, c, ldet, ok, rowbuf, FillOnly<std::remove_reference_t<decltype(fill)>>(fill));
+    panel_ldl_row<NB, FULL, ALG>(BBc, blk, q, c, ldet, ok, rowbuf, FillOnly<std::remove_reference_t<decltype(fill)>>(fill),
+                                 SKIPPAD ? klast : 16);
   };
   // panel row bb over the blocks blk(j), j = bb..NB-1
   auto panel = [&](auto BBc, auto&& blk, auto&& fill) {

@@ -26,6 +26,8 @@
 //    reduce_units (sum over pulsars in pulsar order).
 #include "ewarp_dev.h"
 
+#include <map>
+
 namespace ewh_dev {
 
 thread_local std::string g_err;
@@ -1001,6 +1003,9 @@ struct PsrHost {
   DSpec* d_spec = nullptr;
   int* d_fx_colptr = nullptr;     // fixed CSR (fx_m+1), entries re-indexed
   DSpec* d_fx_spec = nullptr;
+  int* d_fx_rep = nullptr;        // fixed columns -> first column with the same spectrum
+  int* d_fx_ulist = nullptr;      // the distinct-spectrum columns
+  int fx_nu = 0;
   double* d_S = nullptr;          // fx_ld^2
   bool has_theta_white = false;
   int n_slot = 0;
@@ -1215,6 +1220,37 @@ void build_csr_fixed(const ewh_pulsar_desc& s, int nlead, int nloc, int gstart, 
   }
 }
 
+// columns of a CSR whose spectral entries equal (all fields but `col`, bit
+// for bit, same order) those of an earlier column: rep[a] = that column (a
+// itself when first or without entries); ulist = the first columns with
+// entries.  The sin / cos columns of one frequency share a spectrum.
+void build_spec_rep(const std::vector<int>& ptr, const std::vector<DSpec>& ent, std::vector<int>& rep,
+                    std::vector<int>& ulist) {
+  const int ncol = (int)ptr.size() - 1;
+  rep.assign(ncol, 0);
+  ulist.clear();
+  std::map<std::string, int> first;
+  for (int a = 0; a < ncol; ++a) {
+    rep[a] = a;
+    if (ptr[a] == ptr[a + 1]) continue;
+    std::string key;
+    for (int e = ptr[a]; e < ptr[a + 1]; ++e) {
+      DSpec d = ent[e];
+      const int f[5] = {d.kind, d.i0, d.i1, d.i2, 0};
+      const double v[7] = {d.v0, d.v1, d.v2, d.a, d.lnf, d.lnfyr, d.f};
+      key.append((const char*)f, sizeof f);
+      key.append((const char*)v, sizeof v);
+    }
+    auto it = first.find(key);
+    if (it == first.end()) {
+      first.emplace(key, a);
+      ulist.push_back(a);
+    } else {
+      rep[a] = it->second;
+    }
+  }
+}
+
 int dispatch_chol(int mode, int nb, int mreal, const CholJob* jobs, int B, long long u0, long long n, int b_off,
                   const double* theta, int ldth, double* units, hipStream_t st, double* bigscr = nullptr,
                   long long bigcap = 0) {
@@ -1388,7 +1424,8 @@ int setup_fixed(DevCtx* h) {
     // (correlated: the common block is assembled globally), or every column
     // with entries (optimal statistic: the CURN Sigma of each pulsar)
     const int mreal = h->osmode ? ps.fx_ld - 1 : ps.nloc;
-    jobs[p] = CholJob{ps.d_S, 0, ps.fx_ld, mreal, ps.d_fx_colptr, ps.d_fx_spec, h->d_fxK + p, 0, 0};
+    jobs[p] = CholJob{ps.d_S, 0, ps.fx_ld, mreal, ps.d_fx_colptr, ps.d_fx_spec, h->d_fxK + p, 0, 0,
+                      ps.d_fx_rep, ps.d_fx_ulist, ps.fx_nu};
   }
   EWH_HIP(hipMemcpyAsync(fails.data(), h->d_fxfail, sizeof(int) * h->P, hipMemcpyDeviceToHost, h->stream));
   EWH_HIP(hipStreamSynchronize(h->stream));
@@ -1703,6 +1740,14 @@ int create_ctx(const ewh_pta_desc* d, int device, DevCtx** out) {
     build_csr_fixed(s, ps.nlead, ps.nloc, ps.gstart, ps.fx_ld, ptr, ent);
     if ((rc = dupload(h, &ps.d_fx_colptr, ptr.data(), ptr.size()))) return bail(rc);
     if ((rc = dupload(h, &ps.d_fx_spec, ent.data(), ent.size()))) return bail(rc);
+    {
+      std::vector<int> rep, ulist;
+      build_spec_rep(ptr, ent, rep, ulist);
+      ps.fx_nu = (int)ulist.size();
+      if (ulist.empty()) ulist.push_back(0);
+      if ((rc = dupload(h, &ps.d_fx_rep, rep.data(), rep.size()))) return bail(rc);
+      if ((rc = dupload(h, &ps.d_fx_ulist, ulist.data(), ulist.size()))) return bail(rc);
+    }
   }
   h->white_fixed = (d->white_fixed != 0) && !any_theta_white;
   if ((rc = dalloc(h, &h->d_jobs_fixed, h->P))) return bail(rc);
@@ -2131,7 +2176,7 @@ int ewh_set_fixed_white(ewh_handle* H, const double* values) {
 }
 
 int ewh_set_kernel_mode(ewh_handle* H, int32_t mode) {
-  if (!H || mode < 0 || mode > 27) return set_err(EWH_E_INVALID, "bad handle / mode");
+  if (!H || mode < 0 || mode > 29) return set_err(EWH_E_INVALID, "bad handle / mode");
   if (mode >= 3 && mode != 7 && !ab_variants_built())
     return set_err(EWH_E_UNSUPPORTED, "kernel A/B variants are built only into the dev library (make dev)");
   for (DevCtx* h : H->ctx) {
