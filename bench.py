@@ -307,7 +307,7 @@ def main():
                        "parallelism": f"units{world}", "finite_fraction": float(np.mean(np.isfinite(lnl)))},
             "roofline": {"bound": "mfma", "achieved": achieved, "peak": FP64_MFMA_PEAK_TFLOPS, "unit": "TFLOP/s",
                          "frac": achieved / FP64_MFMA_PEAK_TFLOPS, "traffic": traffic,
-                         "kernel": "chol_mfma_kernel<8,1,2,18> (blocked LDL^T panel: diagonal block by fused DPP multiply-adds, row by MFMA with L^-1)", "launch_ms": launch_ms,
+                         "kernel": "chol_mfma_kernel<8,1,2,23> (blocked LDL^T panel: diagonal block by fused DPP multiply-adds, row by MFMA with L^-1)", "launch_ms": launch_ms,
                          "flops_per_launch": flops},
         }
         if cpu is not None:

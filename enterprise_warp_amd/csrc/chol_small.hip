@@ -54,7 +54,7 @@ int launch_chol_small(int mode, int nb, const CholJob* jobs, int B, long long u0
       case 26: launch_chol_mfma<8, 1, 2, 20>(jobs, B, u0, n, b_off, theta, ldth, units, st); return 0;  // default (ALG0 18) + phase stamps
       case 27: launch_chol_mfma<8, 1, 2, 21>(jobs, B, u0, n, b_off, theta, ldth, units, st); return 0;  // default + A22 blocks loaded during phase 1
       case 28: launch_chol_mfma<8, 1, 2, 18>(jobs, B, u0, n, b_off, theta, ldth, units, st); return 0;  // default without the pad-pivot skip
-      case 29: launch_chol_mfma<8, 1, 2, 23>(jobs, B, u0, n, b_off, theta, ldth, units, st); return 0;  // default + each distinct spectrum formed once
+      case 29: launch_chol_mfma<8, 1, 2, 22>(jobs, B, u0, n, b_off, theta, ldth, units, st); return 0;  // default without the spectrum dedupe
       case 21: launch_chol_mfma<8, 1, 2, 15>(jobs, B, u0, n, b_off, theta, ldth, units, st); return 0;  // ALG 11 + phase stamps
       case 20: launch_chol_mfma<8, 1, 2, 14>(jobs, B, u0, n, b_off, theta, ldth, units, st); return 0;  // ALG 11 + staggered first generation
       case 19: launch_chol_mfma<8, 1, 2, 13>(jobs, B, u0, n, b_off, theta, ldth, units, st); return 0;  // + issue order pinned by sched barriers
@@ -69,13 +69,13 @@ int launch_chol_small(int mode, int nb, const CholJob* jobs, int B, long long u0
   // the DPP-mov + fma form --, the rest of the block row by MFMA with L^-1;
   // quotients by one cubic correction of the rcp estimate; phase-3 row scales
   // packed; block row 0 loaded before the spectra; the last panel's pad
-  // pivots skipped: ALG0 22); mode 2:
+  // pivots skipped; each distinct spectrum formed once: ALG0 23); mode 2:
   // the round-1 Cholesky panel (looped) as the A/B baseline
   const bool base = mode == 2;
 #define EWH_CHOL_CASE(NBV)                                                                                   \
   case NBV:                                                                                                  \
     if (base) launch_chol_mfma<NBV, 0, default_waves(NBV), 0>(jobs, B, u0, n, b_off, theta, ldth, units, st); \
-    else launch_chol_mfma<NBV, (NBV <= 8), default_waves(NBV), (NBV <= 8 ? 22 : 1)>(jobs, B, u0, n, b_off, theta, ldth, units, st); \
+    else launch_chol_mfma<NBV, (NBV <= 8), default_waves(NBV), (NBV <= 8 ? 23 : 1)>(jobs, B, u0, n, b_off, theta, ldth, units, st); \
     return 0;
   switch (nb) {
     EWH_CHOL_CASE(1)
