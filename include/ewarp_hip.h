@@ -259,7 +259,7 @@ double ewh_unit_cost(const ewh_handle* h, int32_t pulsar);
  * contraction (varying white noise: separate epoch-sum kernel, unpipelined
  * tiles) instead of the pipelined one and, for a correlated common process,
  * the right-looking dense update and the LDS Gauss-Jordan M_g inverse.
- * Modes 3-6 and 8-16 exist only in the dev library (`make dev`:
+ * Modes 3-6 and 8-29 exist only in the dev library (`make dev`:
  * libewarp_hip_dev.so); the product library returns EWH_E_UNSUPPORTED. */
 int ewh_set_kernel_mode(ewh_handle* h, int32_t mode);
 
