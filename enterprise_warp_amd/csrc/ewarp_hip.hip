@@ -98,6 +98,63 @@ __global__ __launch_bounds__(256) void epoch_sums_kernel(PsrDev P, const double*
 }
 
 // ----------------------------------------------------------------------------
+// fixed white noise, one-off (ewh_create / ewh_set_fixed_white): the cached
+// Gram G = T_aug^T W T_aug - sum_e beta_e s_e s_e^T with every entry summed
+// in double-double (Dot2, Ogita-Rump-Oishi 2005: TwoProd by fma, TwoSum),
+// as if in twice the working precision.  The MFMA contraction sums an entry
+// over up to 20k TOAs in one fp64 accumulator; prior draws whose Sigma is
+// ill-conditioned after the timing-model elimination amplified that rounding
+// to ~1e-1 in lnL on C3 (tests/test_gpu_parity.py::
+// test_c3_bench_workload_prior_draws).  One workgroup per upper 16x16 block,
+// thread (ty, tx) -> entry (16 bi + ty, 16 bj + tx); 32-row TOA chunks staged
+// in LDS.  (Chromatic `vary` bases never take this path: their basis is
+// theta-dependent, so white noise is not cached.)
+__global__ __launch_bounds__(256) void gram_dd_kernel(PsrDev P, const double* __restrict__ w,
+                                                      const double* __restrict__ beta,
+                                                      const double* __restrict__ s, double* __restrict__ G) {
+  const int LD = P.ld, nb = P.nb;
+  int blk = blockIdx.x, bi = 0;
+  while (blk >= nb - bi) { blk -= nb - bi; ++bi; }
+  const int bj = bi + blk;
+  const int tx = threadIdx.x & 15, ty = threadIdx.x >> 4;
+  __shared__ double Ta[32][17], Tb[32][17], wv[32];
+  double hi = 0.0, lo = 0.0;
+  for (int pass = 0; pass < 2; ++pass) {     // TOA rows (w), then epoch rows (-beta)
+    const int nrows = pass == 0 ? P.n_toa : P.n_epoch;
+    const double* src = pass == 0 ? P.T : s;
+    const double* ws = pass == 0 ? w : beta;
+    const double sg = pass == 0 ? 1.0 : -1.0;
+    for (int t0 = 0; t0 < nrows; t0 += 32) {
+      for (int idx = threadIdx.x; idx < 512; idx += 256) {
+        const int r = idx >> 4, cc = idx & 15;
+        const bool in = t0 + r < nrows;
+        Ta[r][cc] = in ? src[(long long)(t0 + r) * LD + 16 * bi + cc] : 0.0;
+        Tb[r][cc] = in ? src[(long long)(t0 + r) * LD + 16 * bj + cc] : 0.0;
+      }
+      if (threadIdx.x < 32) wv[threadIdx.x] = t0 + (int)threadIdx.x < nrows ? sg * ws[t0 + threadIdx.x] : 0.0;
+      __syncthreads();
+      for (int r = 0; r < 32; ++r) {
+        const double x = wv[r] * Ta[r][ty], y = Tb[r][tx];
+        const double p = x * y;
+        const double pe = fma(x, y, -p);            // TwoProd: x y = p + pe exactly
+        const double sum = hi + p;                  // TwoSum: hi + p = sum + se exactly
+        const double bp = sum - hi;
+        const double se = (hi - (sum - bp)) + (p - bp);
+        hi = sum;
+        lo += se + pe;
+      }
+      __syncthreads();
+    }
+  }
+  const int row = 16 * bi + ty, col = 16 * bj + tx;
+  if (row > col) return;      // diagonal block: the upper entry's thread writes both (exactly symmetric)
+  double v = hi + lo;
+  if (row == col && row >= P.m && row < LD - 1) v = 1.0;   // unit pads, as the contraction kernels
+  G[(long long)row * LD + col] = v;
+  G[(long long)col * LD + row] = v;
+}
+
+// ----------------------------------------------------------------------------
 // fixed white noise: eliminate the leading constant-phi (timing-model) block
 // of G once; write the reduced matrix S (fx_ld x fx_ld, r last) and K.
 // One 256-thread block per pulsar; G is modified in place.
@@ -1411,7 +1468,12 @@ int setup_fixed(DevCtx* h) {
                        nullptr);
     if (ps.n_epoch > 0)
       hipLaunchKernelGGL(epoch_sums_kernel, dim3(ps.n_epoch, 1), dim3(256), 0, h->stream, ps.dev, w, nullptr, s);
-    if ((rc = launch_contract_nb(ps.nb, ps.dev, w, beta, s, nullptr, G, 1, h->stream))) return rc;
+    if (ps.dev.n_bgroup == 0 && h->kernel_mode != 7) {
+      hipLaunchKernelGGL(gram_dd_kernel, dim3(ps.nb * (ps.nb + 1) / 2), dim3(256), 0, h->stream, ps.dev, w, beta, s, G);
+      EWH_HIP(hipGetLastError());
+    } else if ((rc = launch_contract_nb(ps.nb, ps.dev, w, beta, s, nullptr, G, 1, h->stream))) {
+      return rc;
+    }
     double Kb_h = 0.0;
     EWH_HIP(hipMemcpyAsync(&Kb_h, Kb, sizeof(double), hipMemcpyDeviceToHost, h->stream));
     EWH_HIP(hipStreamSynchronize(h->stream));
