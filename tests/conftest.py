@@ -90,6 +90,35 @@ def oracle_lnl(pta, X):
     return np.array(out)
 
 
+def orderings_lnl(pta, X):
+    """lnL of every row of X in four correct orderings (enterprise's; the
+    device's factorisation order with a BLAS Gram; reverse-TOA Gram +
+    unblocked Cholesky; the device's order in extended precision) and the
+    measured spread (max - min; 0 where all are -inf, inf where they
+    disagree on -inf).  Returns (vals[4, B], spread[B])."""
+    from oracle.device_order_ref import DeviceOrderPTA
+    from oracle.enterprise_ref import OraclePTA
+    const = pta.constant_values()
+    fixed = const if pta.white_fixed() else None
+    psrs, terms = [c.psr for c in pta.signal_collections], pta.oracle_terms()
+    orcs = [OraclePTA(psrs, terms, fixed_params=fixed),
+            DeviceOrderPTA(psrs, terms, fixed, np.float64, gram_mode="blas"),
+            DeviceOrderPTA(psrs, terms, fixed, np.float64, gram_mode="reverse", factor="chol"),
+            DeviceOrderPTA(psrs, terms, fixed, np.longdouble)]
+    vals = np.empty((len(orcs), len(X)))
+    for i, o in enumerate(orcs):
+        for b, x in enumerate(X):
+            d = dict(const)
+            d.update(pta.map_params(x))
+            vals[i, b] = o.lnlikelihood(d)
+    fin = np.isfinite(vals)
+    spread = np.zeros(len(X))
+    allf = fin.all(axis=0)
+    spread[allf] = vals[:, allf].max(axis=0) - vals[:, allf].min(axis=0)
+    spread[~allf & fin.any(axis=0)] = np.inf
+    return vals, spread
+
+
 def load_golden(name, full=False):
     """Rebuild (pta, theta, lnl, min_eig) from a committed fixture; full=True
     returns (pta, z) with every stored array (lnl_dev, lnl_exact, spread, near)."""

@@ -136,6 +136,21 @@ def test_paramfile_driver_hypermodel(require_gpu, tmp_path, monkeypatch):
     assert X.shape[0] == 32 and np.all(np.isfinite(post))
     out = list(tmp_path.glob("out/**/chain_1.txt"))
     assert len(out) == 1 and np.loadtxt(out[0]).shape[0] == 32 * 3
+    # the final states' lnL against four CPU orderings of the active model
+    # (after 30 steps most chains are still prior-like: measured spread)
+    from conftest import orderings_lnl
+    from enterprise_warp_amd import warp
+    from enterprise_warp_amd.hypermodel import HyperModel
+    hm = HyperModel(warp.init_pta(warp.Params("example_params/default_hypermodel.dat", opts=None)))
+    for k in sorted(set(np.rint(X[:, hm._inm]).astype(int))):
+        sub = hm.models[k]
+        rows = np.flatnonzero(np.rint(X[:, hm._inm]).astype(int) == k)
+        if len(rows) == 0:
+            continue
+        vals, spread = orderings_lnl(sub, X[rows][:, hm._idx[k]])
+        for name, want in zip(("enterprise-order", "device-order", "reverse-chol", "extended"), vals):
+            check_parity(like[rows], want, f"batched driver, model {k} vs {name}", spread=spread,
+                         near=np.zeros(len(rows), bool))
 
 
 def test_ptmcmc_driver_hypermodel(require_gpu, tmp_path, monkeypatch):
