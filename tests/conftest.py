@@ -18,7 +18,7 @@ sys.path.insert(0, ROOT)
 # order extended-precision value (oracle/device_order_ref.py,
 # tests/golden/make_golden.py).  Two correct fp64 orderings of the same
 # likelihood really are that far apart there, so such samples are held to
-# max(strict, SPREAD_K * spread).  DESIGN.md §6.
+# max(strict, SPREAD_K * spread).  DESIGN.md §2.
 ATOL, RTOL = 1e-6, 1e-10
 SPREAD_K = 4.0
 

@@ -2,7 +2,7 @@
 vs the oracle on full-size configurations.  Calls go through the C ABI
 (enterprise_warp_amd.pta.Engine -> ewh_* entry points).
 
-Tolerances (conftest.check_parity, DESIGN.md §6): strict 1e-6 + 1e-10 |lnL|
+Tolerances (conftest.check_parity, DESIGN.md §2): strict 1e-6 + 1e-10 |lnL|
 on every near-truth sample and every full-size check; prior draws of the
 golden fixtures at max(strict, 4 x the spread measured between correct fp64
 orderings of that sample).  No -inf excuse: the -inf pattern must match the
@@ -69,6 +69,9 @@ def test_bilby_bridge_on_device(require_gpu):
             like.parameters = dict(zip(pta.param_names, z["theta"][i]))
             got.append(like.log_likelihood())
         check_parity(np.array(got), z["lnl"][near], name + "/bilby", None, None)
+        # batched form on every golden sample (prior draws: measured spread)
+        batch = like.log_likelihood_batch([dict(zip(pta.param_names, t)) for t in z["theta"]])
+        check_parity(np.asarray(batch), z["lnl"], name + "/bilby batched", z["spread"], z["near"])
 
 
 def test_c2_full_size_vs_oracle(require_gpu):
