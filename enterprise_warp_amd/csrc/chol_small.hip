@@ -55,6 +55,7 @@ int launch_chol_small(int mode, int nb, const CholJob* jobs, int B, long long u0
       case 27: launch_chol_mfma<8, 1, 2, 21>(jobs, B, u0, n, b_off, theta, ldth, units, st); return 0;  // default + A22 blocks loaded during phase 1
       case 28: launch_chol_mfma<8, 1, 2, 18>(jobs, B, u0, n, b_off, theta, ldth, units, st); return 0;  // default without the pad-pivot skip
       case 29: launch_chol_mfma<8, 1, 2, 22>(jobs, B, u0, n, b_off, theta, ldth, units, st); return 0;  // default without the spectrum dedupe
+      case 30: launch_chol_mfma<8, 1, 2, 24>(jobs, B, u0, n, b_off, theta, ldth, units, st); return 0;  // default + A22's first block row loaded before the last phase-1 panel
       case 21: launch_chol_mfma<8, 1, 2, 15>(jobs, B, u0, n, b_off, theta, ldth, units, st); return 0;  // ALG 11 + phase stamps
       case 20: launch_chol_mfma<8, 1, 2, 14>(jobs, B, u0, n, b_off, theta, ldth, units, st); return 0;  // ALG 11 + staggered first generation
       case 19: launch_chol_mfma<8, 1, 2, 13>(jobs, B, u0, n, b_off, theta, ldth, units, st); return 0;  // + issue order pinned by sched barriers

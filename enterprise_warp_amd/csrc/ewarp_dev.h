@@ -1015,7 +1015,7 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(W, W)))
 void chol_mfma_kernel(const CholJob* __restrict__ jobs, int B, long long u0, int b_off,
                       const double* __restrict__ theta, int ldth, double* __restrict__ out_units,
                       double* __restrict__ keep_out, int keep_b0, int keep_bs) {
-  constexpr int ALG = (ALG0 == 14 || ALG0 == 15 || (ALG0 >= 18 && ALG0 <= 23)) ? 11 : ALG0;
+  constexpr int ALG = (ALG0 == 14 || ALG0 == 15 || (ALG0 >= 18 && ALG0 <= 24)) ? 11 : ALG0;
   long long stp[24];
 #ifdef EWH_DEV
 #define EWH_STAMP(I)                                            \
@@ -1064,7 +1064,7 @@ void chol_mfma_kernel(const CholJob* __restrict__ jobs, int B, long long u0, int
   // ALG0 23: each distinct spectrum formed once (J.rep / J.ulist), shared
   // through LDS; every column then takes the same value in the same lane
   // order as before (bit-identical)
-  constexpr bool DEDUP = ALG0 == 23;
+  constexpr bool DEDUP = ALG0 == 23 || ALG0 == 24;
   __shared__ double phs[DEDUP ? LD : 1];
   const bool dedup = DEDUP && J.rep != nullptr;
   if constexpr (DEDUP) {
@@ -1124,7 +1124,7 @@ void chol_mfma_kernel(const CholJob* __restrict__ jobs, int B, long long u0, int
   bool ok = true;
   // LDL^T panel row bb (ALG >= 1)
   // ALG0 22: skip the pad pivots of the last panel (J.mreal .. ld - 2)
-  constexpr bool SKIPPAD = (ALG0 == 22 || ALG0 == 23) && KEEP == 0;
+  constexpr bool SKIPPAD = (ALG0 >= 22 && ALG0 <= 24) && KEEP == 0;
   const int klast = __builtin_amdgcn_readfirstlane(J.mreal - 16 * (NB - 1));
   auto panel_ldl = [&](auto BBc, auto&& blk, auto&& fill) {
     panel_ldl_row<NB, FULL, ALG>(BBc, blk, q, c, ldet, ok, rowbuf, FillOnly<std::remove_reference_t<decltype(fill)>>(fill),
@@ -1188,6 +1188,11 @@ void chol_mfma_kernel(const CholJob* __restrict__ jobs, int B, long long u0, int
   constexpr bool EA = ALG0 == 21 && S::n2 > 0;
   v4d A22[EA ? S::n2 : 1];
   auto ea_count = [](int bb) { return (bb + 1) * H - bb * (bb + 1) / 2; };   // blocks retired by row bb
+  // ALG0 24: only A22's first block row (H, H..NB-1), loaded before the last
+  // phase-1 panel, when rows < H - 1 have retired their (bb, j < H) blocks
+  constexpr bool EAL = ALG0 == 24 && S::n2 > 0 && H >= 2;
+  constexpr int EAN = EAL ? NB - H : 1;
+  v4d A22L[EAN];
   static_for<0, H>([&](auto BI) {
     constexpr int bi = decltype(BI)::value;
     static_for<bi, NB>([&](auto BJ) {
@@ -1234,6 +1239,15 @@ void chol_mfma_kernel(const CholJob* __restrict__ jobs, int B, long long u0, int
       });
     });
     EWH_STAMP(3 + 2 * bb)
+    if constexpr (EAL && bb == H - 2) {
+      static_for<0, EAN>([&](auto T) {
+        constexpr int j = H + decltype(T)::value;
+        static_for<0, 4>([&](auto R) {
+          constexpr int r = decltype(R)::value;
+          A22L[decltype(T)::value][r] = A[(long long)(16 * H + q + 4 * r) * LD + 16 * j + c];
+        });
+      });
+    }
     if constexpr (EA) {
       constexpr int t0 = bb == 0 ? 0 : ((bb * H - (bb - 1) * bb / 2) < S::n2 ? (bb * H - (bb - 1) * bb / 2) : S::n2);
       constexpr int t1 = ((bb + 1) * H - bb * (bb + 1) / 2) < S::n2 ? ((bb + 1) * H - bb * (bb + 1) / 2) : S::n2;
@@ -1254,7 +1268,16 @@ void chol_mfma_kernel(const CholJob* __restrict__ jobs, int B, long long u0, int
     constexpr int i = decltype(II)::value;
     static_for<i, NB>([&](auto JJ) {
       constexpr int j = decltype(JJ)::value;
-      if constexpr (EA) {
+      if constexpr (EAL && i == H) {
+        U2[S::i2(i, j)] = A22L[j - H];
+        if constexpr (i == j) {
+          const double pd = phinv[16 * i + c];
+          static_for<0, 4>([&](auto R) {
+            constexpr int r = decltype(R)::value;
+            U2[S::i2(i, j)][r] += (q + 4 * r == c) ? pd : 0.0;
+          });
+        }
+      } else if constexpr (EA) {
         U2[S::i2(i, j)] = A22[S::i2(i, j)];
         if constexpr (i == j) {
           const double pd = phinv[16 * i + c];

@@ -2238,7 +2238,7 @@ int ewh_set_fixed_white(ewh_handle* H, const double* values) {
 }
 
 int ewh_set_kernel_mode(ewh_handle* H, int32_t mode) {
-  if (!H || mode < 0 || mode > 29) return set_err(EWH_E_INVALID, "bad handle / mode");
+  if (!H || mode < 0 || mode > 30) return set_err(EWH_E_INVALID, "bad handle / mode");
   if (mode >= 3 && mode != 7 && !ab_variants_built())
     return set_err(EWH_E_UNSUPPORTED, "kernel A/B variants are built only into the dev library (make dev)");
   for (DevCtx* h : H->ctx) {
