@@ -9,7 +9,7 @@ template <int NB, int KEEP>
 int launch_partial(const CholJob* jobs, int B, long long u0, long long n, const double* theta, int ldth,
                    double* units, double* keep_out, int keep_bs, hipStream_t st) {
   if constexpr (NB - KEEP >= Split<NB>::H && NB - KEEP >= 0) {
-    hipLaunchKernelGGL(HIP_KERNEL_NAME(chol_mfma_kernel<NB, 0, default_waves(NB), 1, KEEP>),
+    hipLaunchKernelGGL(HIP_KERNEL_NAME(chol_mfma_kernel<NB, default_waves(NB), PANEL_2L, false, KEEP>),
                        dim3((unsigned)n), dim3(64), 0, st, jobs, B, u0, 0, theta, ldth, units, keep_out, 0, keep_bs);
     return 0;
   } else {

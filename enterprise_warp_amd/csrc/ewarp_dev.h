@@ -342,6 +342,10 @@ __global__ __launch_bounds__(256) void contract_mfma_kernel(PsrDev P, const doub
 // ----------------------------------------------------------------------------
 typedef __attribute__((address_space(3))) void lds_void_t;
 typedef __attribute__((address_space(1))) void gbl_void_t;
+// global-address-space view of a device pointer: loads through it are
+// global_load (vmcnt only), not flat_load, whose lgkmcnt share makes every
+// ds_bpermute wait (s_waitcnt lgkmcnt(0)) for all matrix loads in flight
+typedef const __attribute__((address_space(1))) double* gdptr;
 
 // block index blk of the upper triangle (row-major over i <= j) -> (i, j)
 constexpr int tri_i(int nb, int blk) {
@@ -547,16 +551,17 @@ __global__ __launch_bounds__(64 * W) void contract2_kernel(PsrDev P, const doubl
 }
 
 // ----------------------------------------------------------------------------
-// batched Cholesky, MFMA register-blocked: one wave (64 lanes) per unit.
+// batched factorisation, MFMA register-blocked: one wave (64 lanes) per unit.
 // The upper triangle of the LD x LD matrix (LD = 16 NB) is held as 16x16
 // blocks in the v_mfma_f64_16x16x4_f64 C/D layout (lane l, reg r <-> row
-// (l>>4) + 4r, col l&15).  Factor A = U^T U (upper, as LAPACK dpotrf 'U'
-// behind scipy cho_factor).  Per block row bb the 16 pivots of the panel are
-// done by VALU (pivot by readlane, 1/sqrt by v_rsq_f64 + Newton, row k
-// broadcast by ds_bpermute, only the rows that can still change are
-// touched); trailing blocks get A_ij -= U_bi^T U_bj by four MFMAs each with
-// no data movement — register s of a C/D-layout block IS the MFMA A / B
-// operand of k-slice s.
+// (l>>4) + 4r, col l&15).  A = U^T U (upper, as LAPACK dpotrf 'U' behind
+// scipy cho_factor) by a blocked LDL^T: per block row bb the 16x16 diagonal
+// block is eliminated (panel), the rest of the block row becomes
+// V = L^-1 A_bj = E^T A_bj by four MFMAs per block (E = L^-T, built by the
+// panel's column operations), the rows are scaled to U = D^-1/2 V, and the
+// trailing blocks take A_ij -= U_bi^T U_bj by four MFMAs each with no data
+// movement -- register s of a C/D-layout block IS the MFMA A / B operand of
+// k-slice s.
 //
 // Three phases keep at most 26 blocks live for NB = 8 (36 in a plain
 // right-looking order): (1) factor block rows 0..H-1 (H = NB/2) with the
@@ -564,20 +569,15 @@ __global__ __launch_bounds__(64 * W) void contract2_kernel(PsrDev P, const doubl
 // triangle and apply the H panel rows to it; (3) factor A22.  Same
 // arithmetic, re-ordered (left-looking at the 2x2 block level).
 // ----------------------------------------------------------------------------
-template <int NB, int ALG = 0>
+template <int NB>
 struct Split {
-  // block rows of phase 1: NB/2, except 3 of 8 for the unblocked panels
-  // (phase 1's 21 blocks + panel temporaries then fit 256 VGPRs without
-  // spills; phase 2 runs row by row).  The blocked panel (ALG 5) has fewer
-  // panel temporaries and fits at NB/2 = 4 with no scratch (3 spills).
-  static constexpr int H = (NB == 8 && (ALG < 5 || ALG == 9)) ? 3 : NB / 2;
+  static constexpr int H = NB == 8 ? 3 : NB / 2;
   static constexpr int M = NB - H;                    // A22 block order
   static constexpr int n1 = H * NB - H * (H - 1) / 2; // blocks (i < H, j >= i)
   static constexpr int n2 = M * (M + 1) / 2;          // blocks (H <= i <= j)
   static constexpr int i1(int i, int j) { return i * NB - (i * (i - 1)) / 2 + (j - i); }
   static constexpr int i2(int i, int j) { return (i - H) * M - ((i - H) * (i - H - 1)) / 2 + (j - i); }
 };
-
 
 // A -= U_i^T U_j : four f64 MFMAs.  For the f64 MFMAs of gfx940+ the last
 // (blgp) field is the neg modifier (bit 0 negates A: `neg:[1,0,0]`), so no
@@ -587,72 +587,43 @@ __device__ __forceinline__ void syrk_update(v4d& C, const v4d& Ui, const v4d& Uj
   for (int sk = 0; sk < 4; ++sk) C = __builtin_amdgcn_mfma_f64_16x16x4f64(Ui[sk], Uj[sk], C, 0, 0, 1);
 }
 
-// FULL: 1 = every panel step unrolled (large code), 0 = runtime loop over the
-// row's lane group (the default)
-// W: waves per SIMD the register budget is cut for (2 -> 256 VGPRs: the NB = 8
-// three-phase kernel fits with no spills, so two units share each SIMD and one's
-// MFMAs overlap the other's VALU / LDS latency).
-// ALG: panel form.  0 = Cholesky panel (row k scaled by 1/sqrt(pivot) before it
-// is broadcast); 1 = square-root-free LDL^T panel: row k is broadcast raw while
-// 1/d_k is formed, the lane's rows take the update with u_i = A_ki / d_k, and
-// the 16 rows of the block row are scaled to U = D^-1/2 V together at the end
-// (one vector rsqrt per register instead of one serial rsqrt per pivot).  The
-// per-pivot dependency chain drops the scale -> ds_bpermute leg; log|Sigma| =
-// sum log d_k is accumulated per block row from the lanes' own pivots.
-// ALG 5-8 are the blocked panel (diagonal block by VALU, the rest of the row
-// by MFMA with E = L^-T); 6-8 form the pivot quotients by div_fast (one cubic
-// correction), 6 also the row scales by rsqrt_fast (spills), 8 (default)
-// packs the phase-3 row scales into one gather + one rsqrt per block row.
-// LDL^T panel of block row BB over the blocks blk(j), j = BB..NB-1 (C/D
-// layout, upper triangle), used by the register-resident kernels: the 16
-// pivots are factored by VALU (ALG 1: row k broadcast by ds_bpermute, ALG 2:
-// through the per-wave LDS `rowbuf`), then the block row is scaled to
-// U = D^-1/2 V.  Accumulates log d_k (one lane per row) and d_k > 0 per lane.
 // lane (q, c) <- lane (q, K) of its 16-lane row (DPP row_newbcast, gfx90a+):
-// one v_mov_b64_dpp (64-bit DPP takes row_newbcast).  mov_dpp with bound_ctrl
-// has no `old` operand, so no zero is materialised per move (update_dpp(0, ...)
-// on two 32-bit halves cost 2 DPP + 2 v_mov per double).
+// one v_mov_b64_dpp (64-bit DPP takes row_newbcast; with bound_ctrl there is
+// no `old` operand to materialise).
 template <int K>
 __device__ __forceinline__ double row_newbcast(double x) {
   const long v = __builtin_amdgcn_mov_dpp(__builtin_bit_cast(long, x), 0x150 + K, 0xf, 0xf, true);
   return __builtin_bit_cast(double, v);
 }
 
-// the same, only into the 16-lane rows selected by RM (bit q = row q); the
-// other rows read 0 (the `old` operand)
-template <int K, int RM>
-__device__ __forceinline__ double row_newbcast_rows(double x) {
-  const long v = __builtin_amdgcn_update_dpp(0L, __builtin_bit_cast(long, x), 0x150 + K, RM, 0xf, false);
-  return __builtin_bit_cast(double, v);
-}
-
-// One pivot k = 4 KR + KQ of the blocked panel (ALG 11) as fused DP-ALU DPP
-// multiply-adds: the row update A[q+4r][c] += A[q+4r][k] * nw (r > KR; r = KR
-// only in the 16-lane rows q > KQ, by row_mask) and, with DOE, the column
-// operation E[q+4r][c] += E[q+4r][k] * nwm (r <= KR; nwm is 0 in the lanes
-// c <= k), each ONE v_fmac_f64_dpp with src0 read from lane k of its 16-lane
-// row (row_newbcast).  The DPP-mov + fma pairs of ALG 8 compute the same
-// products and sums, so the results are bit-identical; half the VALU issue.
+// One pivot k = 4 KR + KQ of the panel as fused DP-ALU DPP multiply-adds,
+// each ONE v_fmac_f64_dpp whose src0 is read from lane k of its 16-lane row
+// (row_newbcast: column k of the lane's row):
+//  * row update A[q+4r][c] += A[q+4r][k] * nw of register KR in the 16-lane
+//    rows q > KQ (row_mask) and, with FULLROWS (the one-level panel of round
+//    2, dev A/B only), of every register r > KR;
+//  * with DOE the column operation E[q+4r][c] += E[q+4r][k] * nwm on the
+//    registers r <= KR (nwm is 0 in the lanes c <= k).
 // Hazards the compiler cannot see inside the asm: (1) a DPP source must be
 // written >= 2 wait states before it is read -- one statement per pivot, and
 // the next pivot's statement needs nw, whose chain (readlane of this
-// statement's output, rcp, 3 fma) lies in between; pivot 0 follows the
-// compiler's E initialisation, hence its s_nop; (2) E is an MFMA operand (V =
-// E^T A) right after the last column operation (k = 14): a trailing s_nop
-// covers VALU-write -> MFMA-read.  Only live registers (blk, E) are written,
-// so no in-flight MFMA reads them as a dead source.
-// NOP: s_nop 1 first -- pivot 0 (after the compiler's E initialisation) and
-// every pivot of ALG 12, whose statements have no dependency chain between
-// them (the chain runs through row_fmac_bcast).
-template <int K, int KR, int KQ, bool DOE, bool NOP>
+// statement's output, rcp, 3 fma) lies in between; the first pivot of a
+// sub-panel (NOP) follows the compiler's E initialisation or the sub-panel
+// MFMA's copy-out, hence its s_nop; (2) E is an MFMA operand (V = E^T A)
+// right after the last column operation (k = 14): a trailing s_nop covers
+// VALU-write -> MFMA-read.  Only live registers (A, E) are written, so no
+// in-flight MFMA reads them as a dead source.
+template <int K, int KR, int KQ, bool DOE, bool NOP, bool FULLROWS>
 __device__ __forceinline__ void pivot_fused(v4d& A, v4d& E, double nw, double nwm) {
   double a0 = A[0], a1 = A[1], a2 = A[2], a3 = A[3];
   double e0 = E[0], e1 = E[1], e2 = E[2], e3 = E[3];
   constexpr int RM = (0xf << (KQ + 1)) & 0xf;   // rows q > KQ of register KR
   asm(".if %[nop]\n s_nop 1\n .endif\n"
-      ".if %[kr] < 1\n v_fmac_f64_dpp %[a1], %[a1], %[nw] row_newbcast:%[k] row_mask:0xf bank_mask:0xf\n .endif\n"
-      ".if %[kr] < 2\n v_fmac_f64_dpp %[a2], %[a2], %[nw] row_newbcast:%[k] row_mask:0xf bank_mask:0xf\n .endif\n"
-      ".if %[kr] < 3\n v_fmac_f64_dpp %[a3], %[a3], %[nw] row_newbcast:%[k] row_mask:0xf bank_mask:0xf\n .endif\n"
+      ".if %[fr]\n"
+      " .if %[kr] < 1\n v_fmac_f64_dpp %[a1], %[a1], %[nw] row_newbcast:%[k] row_mask:0xf bank_mask:0xf\n .endif\n"
+      " .if %[kr] < 2\n v_fmac_f64_dpp %[a2], %[a2], %[nw] row_newbcast:%[k] row_mask:0xf bank_mask:0xf\n .endif\n"
+      " .if %[kr] < 3\n v_fmac_f64_dpp %[a3], %[a3], %[nw] row_newbcast:%[k] row_mask:0xf bank_mask:0xf\n .endif\n"
+      ".endif\n"
       ".if %[rm] != 0\n"
       " .if %[kr] == 0\n v_fmac_f64_dpp %[a0], %[a0], %[nw] row_newbcast:%[k] row_mask:%[rm] bank_mask:0xf\n .endif\n"
       " .if %[kr] == 1\n v_fmac_f64_dpp %[a1], %[a1], %[nw] row_newbcast:%[k] row_mask:%[rm] bank_mask:0xf\n .endif\n"
@@ -669,17 +640,9 @@ __device__ __forceinline__ void pivot_fused(v4d& A, v4d& E, double nw, double nw
       : [a0] "+v"(a0), [a1] "+v"(a1), [a2] "+v"(a2), [a3] "+v"(a3), [e0] "+v"(e0), [e1] "+v"(e1), [e2] "+v"(e2),
         [e3] "+v"(e3)
       : [nw] "v"(nw), [nwm] "v"(nwm), [k] "i"(K), [kr] "i"(KR), [rm] "i"(RM), [doe] "i"(DOE ? 1 : 0),
-        [nop] "i"(NOP ? 1 : 0));
+        [nop] "i"(NOP ? 1 : 0), [fr] "i"(FULLROWS ? 1 : 0));
   A[0] = a0; A[1] = a1; A[2] = a2; A[3] = a3;
   E[0] = e0; E[1] = e1; E[2] = e2; E[3] = e3;
-}
-
-// x += x[lane k of the 16-lane row] * w (one v_fmac_f64_dpp), after 2 wait
-// states: ALG 12 applies it to the replicated copies of the next two pivot
-// rows, whose sources another such statement may have written just before.
-template <int K>
-__device__ __forceinline__ void row_fmac_bcast(double& x, double w) {
-  asm("s_nop 1\n v_fmac_f64_dpp %0, %0, %1 row_newbcast:%2 row_mask:0xf bank_mask:0xf" : "+v"(x) : "v"(w), "i"(K));
 }
 
 // upper-triangle blocks (i, j), r0 <= i < r1, i <= j < NB, enumerated row by
@@ -700,297 +663,160 @@ constexpr int tri_col(int nb, int r0, int t) {
   return i + t;
 }
 
-struct NoFill {
-  template <typename K>
-  __device__ __forceinline__ void operator()(K) const {}
-  // the blocked panel's E = L^-T of the diagonal block (before V = E^T A) and
-  // each register's row scale D^-1/2: used by the dense diagonal-block kernel
+// Hooks of the panel: the dense diagonal-tile kernel of the correlated
+// factorisation exports E = L^-T of each 16-row sub-block (before V = E^T A)
+// and each register's row scale D^-1/2.
+struct NoHook {
   __device__ __forceinline__ void on_e(const v4d&) const {}
   __device__ __forceinline__ void on_scale(int, double) const {}
 };
 
-// a plain per-pivot filler (lambda) with the no-op hooks
-template <typename F>
-struct FillOnly : NoFill {
-  F& f;
-  __device__ __forceinline__ explicit FillOnly(F& g) : f(g) {}
-  template <typename K>
-  __device__ __forceinline__ void operator()(K k) const { f(k); }
-};
+// Panel forms (template ALG of panel_ldl_row / chol_mfma_kernel):
+//  PANEL_2L (25, the default): two-level.  The 16 pivots of the diagonal
+//    block run in four sub-panels of 4 rows -- register s of the C/D layout.
+//    Inside a sub-panel the pivots update only register s (rows q > kq) and
+//    E; after it, the sub-panel's rows are scaled to U_s = D_s^-1/2 V_s and
+//    the rows below take D -= U_s^T U_s by ONE MFMA (the 16x16x4 shape is
+//    exactly a 4-row rank update).  That update is symmetric by
+//    construction, so the multipliers read from the lower triangle
+//    (A[i][k], i > k) stay equal to the upper entries they stand for.
+//  PANEL_1L (11, dev A/B only: the round-2 default): every pivot updates
+//    every register r >= kr by VALU.  The update A[i][c] -= A[i][k] (A[k][c] /
+//    d) rounds differently from its mirror A[c][i] -= A[c][k] (A[k][i] / d),
+//    so the lower triangle drifts from the upper one and, on ill-conditioned
+//    draws, the Schur complements drift with it (tests/golden: c1_turnover
+//    sample 0 at 4e3x the strict bound vs 22x for PANEL_2L and 79x for
+//    enterprise's LAPACK order).
+constexpr int PANEL_1L = 11;
+constexpr int PANEL_2L = 25;
 
-// fill(integral_constant<k>) runs after pivot k of the diagonal block (ALG >=
-// 5): the lookahead kernel (ALG 10) hands it the independent trailing updates
-// of the previous block row, so their MFMAs issue inside this panel's
-// latency-bound pivot chain instead of after it.
+// The LDL^T panel of block row BB over the blocks blk(j), j = BB..NB-1 (C/D
+// layout, upper triangle; the diagonal block is held in full): eliminates
+// the diagonal block pivot by pivot (row k broadcast to every 16-lane row by
+// ds_bpermute, pivot by readlane, quotient by div_fast), builds E = L^-T by
+// column operations, turns the rest of the row into V = E^T A (4 MFMAs per
+// block) and scales it to U = D^-1/2 V.  Accumulates log d_k (packed: one
+// lane per row) and d_k > 0.
 // RL: the last column of block row NB-1 is the residual (not pivoted), as in
 // the per-pulsar factorisations; false for a plain SPD block (the dense
-// cross-pulsar factorisation's diagonal blocks).
-template <int NB, int FULL, int ALG, bool RL = true, typename BBt, typename Blk, typename Fill = NoFill>
+// cross-pulsar factorisation's diagonal tiles).
+// PACK (PANEL_1L): the row scales D^-1/2 of all 16 rows by one gather + one
+// rsqrt per lane (lane (q, c) takes d of row q + 4 (c/4)); else one per
+// register (the phase-1 form of chol_mfma_kernel<8>, where the packed
+// temporaries spill).  PANEL_2L forms each sub-panel's scales when it closes.
+// klim: pivots >= klim of the last block row are pads (identity rows and
+// columns: pivot 1, every multiplier 0) and are skipped (bit-identical).
+template <int NB, int ALG, bool RL, bool PACK, typename BBt, typename Blk, typename Hook = NoHook>
 __device__ __forceinline__ void panel_ldl_row(BBt BBc, Blk&& blk, int q, int c, LogAcc& ldet, bool& ok,
-                                              double* rowbuf, Fill&& fill = Fill{}, int klim = 16) {
-  constexpr int LD = 16 * NB;
-  (void)rowbuf;
-  (void)LD;
+                                              const Hook& hook = Hook{}, int klim = 16) {
   constexpr int bb = decltype(BBc)::value;
-  static_assert(ALG < 3 || FULL, "the DPP panel needs compile-time pivots");
-  if constexpr (ALG >= 5) {
-    // ALG 16/17: the pivots run at raised wave priority, so their dependent
-    // VALU chain is not starved by the partner wave's back-to-back MFMAs
-    constexpr bool PRIO = ALG == 16 || ALG == 17;
-    if constexpr (PRIO) __builtin_amdgcn_s_setprio(2);
-    // ALG 5 (blocked panel): eliminate the 16x16 diagonal block alone (rows >
-    // k take row k, u_i from its symmetric lower part by DPP as ALG 3/4)
-    // while E = L^-T accumulates the matching COLUMN operations
-    //   col c -= u_c col k  (c > k),  u_c = A[k][c] / d_k = rk_bb[c] / d_k
-    // (column k of E is an intra-row DPP broadcast, u_c is the row-k value
-    // this lane already holds: no LDS).  The off-diagonal blocks of the row
-    // then take V_bj = L^-1 A_bj = E^T A_bj by four MFMAs each instead of 16
-    // rank-1 VALU steps and 16 row broadcasts (2 ds_bpermute per double).
-    v4d E;
-    static_for<0, 4>([&](auto R) {
-      constexpr int r = decltype(R)::value;
-      E[r] = (q + 4 * r == c) ? 1.0 : 0.0;
-    });
-    // ALG 12: R = pivot row k, replicated over the four 16-lane row groups
-    // (R[c] = A[k][c] in every lane of column c); R1, R2 = the next two rows as
-    // they stood before this pivot.  Pivot k turns R1 into the next R and
-    // brings R2 up to date by the same fused multiply-add the block rows
-    // take; the row after them is fetched by ds_bpermute right after the
-    // block-row update and is not needed for two pivots, so the per-pivot
-    // dependency chain (R -> d, 1/d -> nw -> R1) has no LDS round trip.
-    constexpr int NPIV = (RL && bb == NB - 1) ? 15 : 16;
-    // ALG 13: the same with the issue order pinned by scheduling barriers:
-    // nw, then R1 and the next pivot's readlane, then the rest of the pivot.
-    constexpr bool RP = ALG == 12 || ALG == 13;
-    double R = 0.0, R1 = 0.0, R2 = 0.0, dn = 0.0;
-    if constexpr (RP) {
-      R = __shfl(blk(BBc)[0], c);
-      R1 = __shfl(blk(BBc)[0], 16 + c);
-      R2 = __shfl(blk(BBc)[0], 32 + c);
-      dn = readlane_d(R, 0);
-    }
-    static_for<0, 4>([&](auto KR) {
-      constexpr int kr = decltype(KR)::value;
-      constexpr int nk = (RL && bb == NB - 1 && kr == 3) ? 3 : 4;   // the r column is not pivoted
-      static_for<0, nk>([&](auto KQc) {
-        constexpr int kq = decltype(KQc)::value;
-        constexpr int k = 4 * kr + kq;
-        if constexpr ((ALG >= 11 && ALG <= 13) || ALG == 16 || ALG == 17) {
-          // the last panel's pad columns (k >= klim, wave-uniform: identity rows
-          // and columns, pivot 1, every multiplier 0) are no-ops: skipped, and
-          // the result is bit-identical
-          if constexpr (ALG == 11 && RL && bb == NB - 1) {
-            if (k >= klim) {
-              fill(std::integral_constant<int, k>{});
-              return;
-            }
-          }
-          // fused DPP multiply-adds (pivot_fused): nw = -A[k][c] / d_k, the
-          // column operations take it only in the lanes c > k
-          constexpr bool doe = (bb < NB - 1 || !RL) && k < 15;
-          constexpr bool nxt = RP && k + 1 < NPIV;
-          const double xk = RP ? R : __shfl(blk(BBc)[kr], 16 * kq + c);
-          const double d = RP ? dn : readlane_d(blk(BBc)[kr], 16 * kq + k);
-          const double nw = div_fast(-xk, d);
-          if constexpr (nxt) {
-            row_fmac_bcast<k>(R1, nw);
-            dn = readlane_d(R1, k + 1);
-          }
-          if constexpr (ALG == 13) __builtin_amdgcn_sched_barrier(0);
-          const double nwm = (doe && c > k) ? nw : 0.0;
-          if constexpr (RP && k + 2 < NPIV) row_fmac_bcast<k>(R2, nw);
-          pivot_fused<k, kr, kq, doe, (k == 0 || RP)>(blk(BBc), E, nw, nwm);
-          if constexpr (nxt) {
-            R = R1;
-            R1 = R2;
-            if constexpr (k + 3 < NPIV) R2 = __shfl(blk(BBc)[(k + 3) / 4], 16 * ((k + 3) % 4) + c);
-          }
-          if constexpr (ALG == 13) __builtin_amdgcn_sched_barrier(0);
-          fill(std::integral_constant<int, k>{});
-          return;
-        }
-        const double d = readlane_d(blk(BBc)[kr], 16 * kq + k);
-        // raw multipliers A[q + 4r][k] (rows > k): register kr only in the
-        // 16-lane rows q > kq (DPP row_mask; disabled rows read 0)
-        double ui[4];
-        static_for<kr + 1, 4>([&](auto R) {
-          constexpr int r = decltype(R)::value;
-          ui[r] = row_newbcast<k>(blk(BBc)[r]);
-        });
-        if constexpr (kq < 3) ui[kr] = row_newbcast_rows<k, (0xf << (kq + 1)) & 0xf>(blk(BBc)[kr]);
-        // w = A[k][c] / d_k: the row-k value of this lane's column, scaled once
-        // (ALG >= 6: the quotient by div_fast -- one op and ~12 cycles of the
-        // per-pivot chain less; ALG 6 also scales the rows by rsqrt_fast,
-        // which makes this kernel spill 68 bytes per lane, ALG 7 does not)
-        const double xk = __shfl(blk(BBc)[kr], 16 * kq + c);
-        const double w = ALG >= 6 ? div_fast(xk, d) : xk * rcp_nr(d);
-        static_for<(kq < 3 ? kr : kr + 1), 4>([&](auto R) {
-          constexpr int r = decltype(R)::value;
-          blk(BBc)[r] = fma(-ui[r], w, blk(BBc)[r]);
-        });
-        if constexpr ((bb < NB - 1 || !RL) && k < 15) {
-          const double uc = (c > k) ? w : 0.0;
-          static_for<0, kr + 1>([&](auto R) {
-            constexpr int r = decltype(R)::value;
-            E[r] = fma(-uc, row_newbcast<k>(E[r]), E[r]);
-          });
-        }
-        fill(std::integral_constant<int, k>{});
-      });
-    });
-    if constexpr (PRIO) __builtin_amdgcn_s_setprio(0);
-    if constexpr (bb < NB - 1 || !RL) fill.on_e(E);
-    static_for<bb + 1, NB>([&](auto JJ) {
-      v4d acc = {0.0, 0.0, 0.0, 0.0};
-      static_for<0, 4>([&](auto S) {
-        constexpr int s = decltype(S)::value;
-        acc = __builtin_amdgcn_mfma_f64_16x16x4f64(E[s], blk(JJ)[s], acc, 0, 0, 0);
-      });
-      blk(JJ) = acc;
-    });
-  } else
+  constexpr bool TWO = ALG == PANEL_2L;
+  static_assert(ALG == PANEL_1L || ALG == PANEL_2L, "unknown panel form");
+  constexpr bool LASTR = RL && bb == NB - 1;          // block row holding the residual
+  v4d E;
+  static_for<0, 4>([&](auto R) {
+    constexpr int r = decltype(R)::value;
+    E[r] = (q + 4 * r == c) ? 1.0 : 0.0;
+  });
+  // two-level: the row scales D^-1/2 of sub-panel s, formed when it closes
+  double rsr[4] = {1.0, 1.0, 1.0, 1.0};
   static_for<0, 4>([&](auto KR) {
     constexpr int kr = decltype(KR)::value;
-    // ALG 3: u_i = A[q + 4r][k] read from the SYMMETRIC lower part of the
-    // diagonal block (lane (q, k), register r: kept exact by the full-block
-    // updates) with one DPP row broadcast per register -- no ds_bpermute
-    auto step3 = [&](auto KQc) {
+    constexpr int nk = (LASTR && kr == 3) ? 3 : 4;   // the r column is not pivoted
+    static_for<0, nk>([&](auto KQc) {
       constexpr int kq = decltype(KQc)::value;
       constexpr int k = 4 * kr + kq;
+      if constexpr (LASTR) {
+        if (k >= klim) return;                         // wave-uniform: pad pivots
+      }
+      constexpr bool doe = !LASTR && k < 15;
+      const double xk = __shfl(blk(BBc)[kr], 16 * kq + c);    // A[k][c]
       const double d = readlane_d(blk(BBc)[kr], 16 * kq + k);
-      double ui[4];
-      double rk[NB];
-      static_for<kr, 4>([&](auto R) {
-        constexpr int r = decltype(R)::value;
-        const double v = row_newbcast<k>(blk(BBc)[r]);
-        ui[r] = (ALG == 4 || r > kr || q > kq) ? v : 0.0;
-      });
-      static_for<bb, NB>([&](auto JJ) {
-        constexpr int j = decltype(JJ)::value;
-        rk[j] = __shfl(blk(JJ)[kr], 16 * kq + c);   // (a permlane32/16_swap broadcast measured 1.43x slower)
-      });
-      const double dinv = rcp_nr(d);
-      static_for<kr, 4>([&](auto R) { ui[decltype(R)::value] *= dinv; });
-      static_for<bb, NB>([&](auto JJ) {
-        constexpr int j = decltype(JJ)::value;
-        static_for<(ALG == 4 ? kr + 1 : kr), 4>([&](auto R) {
-          constexpr int r = decltype(R)::value;
-          blk(JJ)[r] = fma(-ui[r], rk[j], blk(JJ)[r]);
-        });
-      });
-      // ALG 4: register kr holds rows 4 kr + q and only rows below the pivot
-      // (q > kq) change -- an exec-masked branch (SALU) instead of a select on u_i
-      if constexpr (ALG == 4) {
-        if (q > kq) {
-          static_for<bb, NB>([&](auto JJ) {
-            constexpr int j = decltype(JJ)::value;
-            blk(JJ)[kr] = fma(-ui[kr], rk[j], blk(JJ)[kr]);
-          });
+      const double nw = div_fast(-xk, d);
+      const double nwm = (doe && c > k) ? nw : 0.0;
+      pivot_fused<k, kr, kq, doe, (TWO ? kq == 0 : k == 0), !TWO>(blk(BBc), E, nw, nwm);
+    });
+    if constexpr (TWO) {
+      // sub-panel kr done: lane (q, c) takes the pivot of row 4 kr + q (lane
+      // (q, 4 kr + q)): log-det, positivity, row scale; U_s = D_s^-1/2 V_s and
+      // the rows below take D -= U_s^T U_s (one MFMA, in place: registers
+      // <= kr are not read again)
+      auto sub = [&]() {
+        const double dg = __shfl(blk(BBc)[kr], 17 * q + 4 * kr);
+        const double dv = (LASTR && kr == 3 && q == 3) ? 1.0 : dg;   // (the r row)
+        ok = ok && (dv > 0.0);
+        if (c == 0) ldet.add(dv);
+        if constexpr (!(LASTR && kr == 3)) {
+          const double rs = rsqrt_fast(dv);
+          rsr[kr] = rs;
+          if constexpr (kr < 3) {
+            const double u = blk(BBc)[kr] * rs;
+            blk(BBc) = __builtin_amdgcn_mfma_f64_16x16x4f64(u, u, blk(BBc), 0, 0, 1);
+          }
         }
-      }
-    };
-    auto step = [&](const int kq) {
-      const int k = 4 * kr + kq;
-      const double d = readlane_d(blk(BBc)[kr], 16 * kq + k);            // wave-uniform pivot
-      // raw row k: A[k][q + 4r] for this lane's rows (masked to rows > k) and
-      // A[k][col c] of every block of the row; both in flight while 1/d forms
-      double ui[4];
-      double rk[NB];
-      if constexpr (ALG == 2) {
-        // LDS broadcast: the 16 lanes of quad kq store row k of every block
-        // (one ds_write_b64 per block), every lane reads it back with 16
-        // distinct addresses per read (broadcast, bank-conflict free) --
-        // several times cheaper on the CU's LDS than two ds_bpermute_b32
-        // per double.  One wave per workgroup and LDS ops of a wave run in
-        // order, so no barrier: the asm fences only stop the compiler from
-        // moving the reads above the other lanes' writes.
-        double* rb = rowbuf + (k & 1) * LD;
-        if (q == kq) {
-          static_for<bb, NB>([&](auto JJ) {
-            constexpr int j = decltype(JJ)::value;
-            rb[16 * j + c] = blk(JJ)[kr];
-          });
-        }
-        asm volatile("" ::: "memory");
-        static_for<kr, 4>([&](auto R) {
-          constexpr int r = decltype(R)::value;
-          const double v = rb[16 * bb + q + 4 * r];
-          ui[r] = (r > kr || q > kq) ? v : 0.0;
-        });
-        static_for<bb, NB>([&](auto JJ) {
-          constexpr int j = decltype(JJ)::value;
-          rk[j] = rb[16 * j + c];
-        });
-        asm volatile("" ::: "memory");
+      };
+      if constexpr (LASTR) {
+        if (4 * kr < klim) sub();                      // (a sub-panel of pads: pivots 1, no update)
       } else {
-        static_for<kr, 4>([&](auto R) {
-          constexpr int r = decltype(R)::value;
-          const double v = __shfl(blk(BBc)[kr], 16 * kq + q + 4 * r);
-          ui[r] = (r > kr || q > kq) ? v : 0.0;
-        });
-        static_for<bb, NB>([&](auto JJ) {
-          constexpr int j = decltype(JJ)::value;
-          rk[j] = __shfl(blk(JJ)[kr], 16 * kq + c);
-        });
+        sub();
       }
-      const double dinv = rcp_nr(d);
-      static_for<kr, 4>([&](auto R) { ui[decltype(R)::value] *= dinv; });
-      static_for<bb, NB>([&](auto JJ) {
-        constexpr int j = decltype(JJ)::value;
-        static_for<kr, 4>([&](auto R) {
-          constexpr int r = decltype(R)::value;
-          blk(JJ)[r] = fma(-ui[r], rk[j], blk(JJ)[r]);
-        });
-      });
-    };
-    constexpr int nk = (bb == NB - 1 && kr == 3) ? 3 : 4;   // the r column is not pivoted
-    if constexpr (ALG >= 3) {
-      static_for<0, nk>([&](auto KQ) { step3(KQ); });
-    } else if constexpr (FULL) {
-      static_for<0, nk>([&](auto KQ) {
-        step(decltype(KQ)::value);
-        // unrolled LDS-broadcast steps: keep the scheduler from hoisting the
-        // next steps' LDS reads (it otherwise spills ~1 KB per lane)
-        if constexpr (ALG == 2) __builtin_amdgcn_sched_barrier(0);
-      });
-    } else {
-#pragma unroll 1
-      for (int kq = 0; kq < nk; ++kq) step(kq);
     }
   });
-  // rows of the block row -> U = d^-1/2 V, d of row q + 4r read from the
-  // diagonal (lane 17q + 4r); log-det and positivity from one lane per row
-  // (c == 0); the r row (last block, row 15) is left as it is
-  if constexpr (((ALG == 8 || ALG >= 10) && bb >= Split<NB, ALG>::H) || ALG == 9) {
-    // (phase 3 only: in phase 1 the extra temporaries spill)
-    // packed: lane (q, c) takes d of row q + 4 (c/4) -- held in register c/4
-    // of lane (q, q + 4 (c/4)), whose own c/4 is the same -- so one gather,
-    // one rsqrt and one log-det term (lanes c % 4 == 0) cover all 16 rows;
-    // register r then takes its rows' scale from lane (q, 4r) by DPP
+  if constexpr (!LASTR) hook.on_e(E);
+  static_for<bb + 1, NB>([&](auto JJ) {
+    v4d acc = {0.0, 0.0, 0.0, 0.0};
+    static_for<0, 4>([&](auto S) {
+      constexpr int s = decltype(S)::value;
+      acc = __builtin_amdgcn_mfma_f64_16x16x4f64(E[s], blk(JJ)[s], acc, 0, 0, 0);
+    });
+    blk(JJ) = acc;
+  });
+  // rows of the block row -> U = d^-1/2 V (the diagonal block itself is not
+  // needed after its panel; the last block row has nothing to scale)
+  if constexpr (TWO) {
+    if constexpr (!LASTR) {
+      static_for<0, 4>([&](auto R) {
+        constexpr int r = decltype(R)::value;
+        hook.on_scale(r, rsr[r]);
+        static_for<bb + 1, NB>([&](auto JJ) { blk(JJ)[r] *= rsr[r]; });
+      });
+    }
+  } else if constexpr (PACK) {
+    // d of row q + 4r read from the diagonal (lane 17q + 4r); lane (q, c)
+    // takes d of row q + 4 (c/4) -- held in register c/4 of lane
+    // (q, q + 4 (c/4)), whose own c/4 is the same -- so one gather, one rsqrt
+    // and one log-det term (lanes c % 4 == 0) cover all 16 rows; register r
+    // then takes its rows' scale from lane (q, 4r) by DPP
     const int cr = c >> 2;
     const double own = cr == 0 ? blk(BBc)[0] : cr == 1 ? blk(BBc)[1] : cr == 2 ? blk(BBc)[2] : blk(BBc)[3];
     double dv = __shfl(own, 17 * q + 4 * cr);
-    if constexpr (RL && bb == NB - 1) dv = (q == 3 && cr == 3) ? 1.0 : dv;
+    if constexpr (LASTR) dv = (q == 3 && cr == 3) ? 1.0 : dv;
     ok = ok && (dv > 0.0);
     if ((c & 3) == 0) ldet.add(dv);
-    const double rsp = rsqrt_nr(dv);
+    if constexpr (!LASTR) {
+      const double rsp = rsqrt_nr(dv);
+      static_for<0, 4>([&](auto R) {
+        constexpr int r = decltype(R)::value;
+        const double rs = row_newbcast<4 * r>(rsp);
+        hook.on_scale(r, rs);
+        static_for<bb + 1, NB>([&](auto JJ) { blk(JJ)[r] *= rs; });
+      });
+    }
+  } else {
     static_for<0, 4>([&](auto R) {
       constexpr int r = decltype(R)::value;
-      const double rs = row_newbcast<4 * r>(rsp);
-      static_for<bb, NB>([&](auto JJ) { blk(JJ)[r] *= rs; });
+      const bool rrow = LASTR && r == 3 && q == 3;
+      const double dg = __shfl(blk(BBc)[r], 17 * q + 4 * r);
+      const double dv = rrow ? 1.0 : dg;
+      ok = ok && (dv > 0.0);
+      if (c == 0) ldet.add(dv);
+      if constexpr (!LASTR) {
+        const double rs = rsqrt_nr(dv);
+        hook.on_scale(r, rs);
+        static_for<bb + 1, NB>([&](auto JJ) { blk(JJ)[r] *= rs; });
+      }
     });
-  } else
-  static_for<0, 4>([&](auto R) {
-    constexpr int r = decltype(R)::value;
-    const bool rrow = RL && (bb == NB - 1 && r == 3) && q == 3;
-    const double dg = __shfl(blk(BBc)[r], 17 * q + 4 * r);
-    const double dv = rrow ? 1.0 : dg;
-    ok = ok && (dv > 0.0);
-    if (c == 0) ldet.add(dv);
-    const double rs = rrow ? 1.0 : (ALG == 6 ? rsqrt_fast(dv) : rsqrt_nr(dv));
-    fill.on_scale(r, rs);
-    static_for<bb, NB>([&](auto JJ) { blk(JJ)[r] *= rs; });
-  });
+  }
 }
 
 // KEEP > 0 (correlated common process): only block rows 0..NB-KEEP-1 (the
@@ -1001,108 +827,87 @@ __device__ __forceinline__ void panel_ldl_row(BBt BBc, Blk&& blk, int q, int c, 
 // all-gather moves), and
 // the unit term is the local part K - 1/2 log|Sigma_LL| - 1/2 log|phi_L|.
 #ifdef EWH_DEV
-// ALG0 15 (dev diagnostics): ALG 11 with s_memtime stamps at the phase
-// boundaries of the units with blockIdx < STAMP_UNITS (ewh_dev_stamps)
+// STAMP (dev diagnostics): s_memtime stamps at the phase boundaries of the
+// units with blockIdx < STAMP_UNITS (ewh_dev_stamps)
 constexpr int STAMP_UNITS = 4096, STAMP_N = 24;
 static __device__ long long g_stamps[STAMP_UNITS * STAMP_N];
 #endif
 
-// ALG0 14 (A/B): ALG 11 with the first generation of units started at
-// scattered times (0-3k cycles), so the two units sharing a SIMD do not run
-// their latency-bound panels in lockstep.
-template <int NB, int FULL, int W, int ALG0 = 0, int KEEP = 0>
+// W: waves per SIMD the register budget is cut for (2 -> 256 VGPRs: the NB = 8
+// three-phase kernel fits, so two units share each SIMD and one's MFMAs
+// overlap the other's VALU / LDS latency).  Block row 0 is loaded before the
+// spectra are formed (its latency overlaps the prologue); with fixed white
+// noise each distinct spectrum is formed once (the sin / cos columns of a
+// frequency share one: J.rep / J.ulist) and shared through LDS; the last
+// panel's pad pivots are skipped.
+template <int NB, int W, int ALG = PANEL_2L, bool STAMP = false, int KEEP = 0>
 __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(W, W)))
 void chol_mfma_kernel(const CholJob* __restrict__ jobs, int B, long long u0, int b_off,
                       const double* __restrict__ theta, int ldth, double* __restrict__ out_units,
                       double* __restrict__ keep_out, int keep_b0, int keep_bs) {
-  constexpr int ALG = (ALG0 == 14 || ALG0 == 15 || (ALG0 >= 18 && ALG0 <= 24)) ? 11 : ALG0;
-  long long stp[24];
 #ifdef EWH_DEV
+  long long stp[STAMP_N];
 #define EWH_STAMP(I)                                            \
-  if constexpr (ALG0 == 15 || ALG0 == 20) {                     \
+  if constexpr (STAMP) {                                        \
     __builtin_amdgcn_sched_barrier(0);                          \
     stp[(I)] = (long long)__builtin_amdgcn_s_memtime();         \
     __builtin_amdgcn_sched_barrier(0);                          \
   }
 #else
+  static_assert(!STAMP, "phase stamps exist only in the dev library");
 #define EWH_STAMP(I)
 #endif
   EWH_STAMP(0)
-  if constexpr (ALG0 == 17) __builtin_amdgcn_s_setprio(2);
-  if constexpr (ALG0 == 14) {
-    if (blockIdx.x < 2048) {
-      const unsigned n = (blockIdx.x * 2654435761u >> 26) % 48u;
-      for (unsigned i = 0; i < n; ++i) __builtin_amdgcn_s_sleep(1);
-    }
-  }
   constexpr int LD = 16 * NB;
-  using S = Split<NB, ALG>;
+  using S = Split<NB>;
   constexpr int H = S::H;
   static_assert(NB - KEEP >= H, "kept blocks must lie in the phase-3 triangle");
   __shared__ double phinv[LD];
-  __shared__ double rowbuf[ALG == 2 ? 2 * LD : 1];   // ALG 2: double-buffered row-k broadcast
+  __shared__ double phs[LD];
   const int lane = threadIdx.x;
   const int q = lane >> 4, c = lane & 15;
   const long long u = u0 + xcd_unit(blockIdx.x, gridDim.x);
   const int p = (int)(u / B), b = (int)(u % B);
   const CholJob J = jobs[p];
-  const double* A = J.mats + (long long)(b - b_off) * J.mstride;
+  const gdptr A = (gdptr)(J.mats + (long long)(b - b_off) * J.mstride);
   const double* th = theta + (long long)b * ldth;
 
-  // ALG0 18: block row 0 of the matrix is loaded before the spectra are
-  // formed, so its latency overlaps the prologue (phinv is added after)
-  constexpr bool PRE = ALG0 == 18 || ALG0 >= 20;
-  v4d pre[PRE ? NB : 1];
-  if constexpr (PRE) {
-    static_for<0, NB>([&](auto BJ) {
-      static_for<0, 4>([&](auto R) {
-        constexpr int r = decltype(R)::value;
-        pre[decltype(BJ)::value][r] = A[(long long)(q + 4 * r) * LD + 16 * decltype(BJ)::value + c];
-      });
+  v4d pre[NB];
+  static_for<0, NB>([&](auto BJ) {
+    static_for<0, 4>([&](auto R) {
+      constexpr int r = decltype(R)::value;
+      pre[decltype(BJ)::value][r] = A[(long long)(q + 4 * r) * LD + 16 * decltype(BJ)::value + c];
     });
-  }
-  // ALG0 23: each distinct spectrum formed once (J.rep / J.ulist), shared
-  // through LDS; every column then takes the same value in the same lane
-  // order as before (bit-identical)
-  constexpr bool DEDUP = ALG0 == 23 || ALG0 == 24;
-  __shared__ double phs[DEDUP ? LD : 1];
-  const bool dedup = DEDUP && J.rep != nullptr;
-  if constexpr (DEDUP) {
-    if (dedup) {
-      for (int i = lane; i < J.nu; i += 64) {
-        const int a = J.ulist[i];
-        double ph = 0.0;
-        for (int e = J.col_ptr[a]; e < J.col_ptr[a + 1]; ++e) ph += spec_phi_body(J.spec[e], th);
-        phs[a] = ph;
-      }
-      __syncthreads();
+  });
+  const bool dedup = J.rep != nullptr;
+  if (dedup) {
+    for (int i = lane; i < J.nu; i += 64) {
+      const int a = J.ulist[i];
+      double ph = 0.0;
+      for (int e = J.col_ptr[a]; e < J.col_ptr[a + 1]; ++e) ph += spec_phi_body(J.spec[e], th);
+      phs[a] = ph;
     }
+    __syncthreads();
   }
-  LogAcc lphi;
+  // log|phi| is summed into the per-lane log-det accumulator (one log() at
+  // the end of the kernel)
+  LogAcc ldet;
   for (int a = lane; a < LD; a += 64) {
     double pi = 0.0;
     if (a < J.mreal && J.col_ptr[a] < J.col_ptr[a + 1]) {   // (pads carry no entry)
       double ph = 0.0;
-      if constexpr (ALG0 == 19) {
-        ph = 1.0 + 1e-3 * a;   // diagnostic: no spectra (wrong values)
-      } else if (dedup) {
+      if (dedup) {
         ph = phs[J.rep[a]];
       } else {
         for (int e = J.col_ptr[a]; e < J.col_ptr[a + 1]; ++e) ph += spec_phi_body(J.spec[e], th);
       }
       pi = 1.0 / ph;
-      lphi.add(ph);
+      ldet.add(ph);
     }
     phinv[a] = pi;
   }
-  // ALG >= 1 sums log|phi| into the per-lane log-det accumulator below, so
-  // the kernel takes a single log() at its end (two calls let the compiler
-  // keep the polynomial constants of the first one live across the whole
-  // factorisation: spilled to scratch and reloaded serially at the end)
-  const double lphi_sum = ALG >= 1 ? 0.0 : wave_sum(lphi.value());
   __syncthreads();
   EWH_STAMP(1)
-  if constexpr (ALG0 == 17) __builtin_amdgcn_s_setprio(0);
 
   auto load_block = [&](auto BI, auto BJ, v4d& v) {
     constexpr int bi = decltype(BI)::value, bj = decltype(BJ)::value;
@@ -1119,85 +924,19 @@ void chol_mfma_kernel(const CholJob* __restrict__ jobs, int B, long long u0, int
     }
   };
 
-  LogAcc ldet;
-  if constexpr (ALG >= 1) ldet = lphi;
   bool ok = true;
-  // LDL^T panel row bb (ALG >= 1)
-  // ALG0 22: skip the pad pivots of the last panel (J.mreal .. ld - 2)
-  constexpr bool SKIPPAD = (ALG0 >= 22 && ALG0 <= 24) && KEEP == 0;
-  const int klast = __builtin_amdgcn_readfirstlane(J.mreal - 16 * (NB - 1));
-  auto panel_ldl = [&](auto BBc, auto&& blk, auto&& fill) {
-    panel_ldl_row<NB, FULL, ALG>(BBc, blk, q, c, ldet, ok, rowbuf, FillOnly<std::remove_reference_t<decltype(fill)>>(fill),
-                                 SKIPPAD ? klast : 16);
-  };
-  // panel row bb over the blocks blk(j), j = bb..NB-1
-  auto panel = [&](auto BBc, auto&& blk, auto&& fill) {
-    if constexpr (ALG >= 1) {
-      panel_ldl(BBc, blk, fill);
-      return;
-    }
-    constexpr int bb = decltype(BBc)::value;
-    static_for<0, 4>([&](auto KR) {
-      constexpr int kr = decltype(KR)::value;
-      auto step = [&](const int kq) {
-        const int k = 4 * kr + kq;
-        const double piv = readlane_d(blk(BBc)[kr], 16 * kq + k);           // wave-uniform
-        ok = ok && (piv > 0.0);
-        ldet.add(piv);
-        const double rin = rsqrt_nr(piv);
-        const double sc = (q == kq) ? rin : 1.0;                             // scales row k only
-        const double xbb = blk(BBc)[kr] * sc;
-        // U[k][q + 4r] for this lane's rows; rows <= k are final (r < kr never
-        // changes, r == kr only for q > kq)
-        double ui[4];
-        static_for<kr, 4>([&](auto R) {
-          constexpr int r = decltype(R)::value;
-          const double v = __shfl(xbb, 16 * kq + q + 4 * r);
-          ui[r] = (r > kr || q > kq) ? v : 0.0;
-        });
-        double rk[NB];
-        static_for<bb, NB>([&](auto JJ) {
-          constexpr int j = decltype(JJ)::value;
-          const double x = (j == bb) ? xbb : blk(JJ)[kr] * sc;
-          blk(JJ)[kr] = x;
-          rk[j] = __shfl(x, 16 * kq + c);                                    // U[k][col c] of block (bb, j)
-        });
-        static_for<bb, NB>([&](auto JJ) {
-          constexpr int j = decltype(JJ)::value;
-          static_for<kr, 4>([&](auto R) {
-            constexpr int r = decltype(R)::value;
-            blk(JJ)[r] = fma(-ui[r], rk[j], blk(JJ)[r]);
-          });
-        });
-      };
-      constexpr int nk = (bb == NB - 1 && kr == 3) ? 3 : 4;   // the r column is not pivoted
-      if constexpr (FULL) {
-        static_for<0, nk>([&](auto KQ) { step(decltype(KQ)::value); });
-      } else {
-#pragma unroll 1
-        for (int kq = 0; kq < nk; ++kq) step(kq);
-      }
-    });
-  };
+  constexpr bool SKIPPAD = KEEP == 0;
+  const int klast = SKIPPAD ? __builtin_amdgcn_readfirstlane(J.mreal - 16 * (NB - 1)) : 16;
+  // phase 1 (NB = 8): per-register row scales (the packed form's temporaries spill there)
+  constexpr bool PACK1 = NB != 8;
 
   // ---- phase 1: block rows 0..H-1 ----
   v4d U1[S::n1 > 0 ? S::n1 : 1];
-  // ALG0 21: the A22 blocks phase 2 starts from are loaded during phase 1, a
-  // few after each trailing update -- as many as that update retired (the
-  // blocks (bb, j < H) are dead once rows < H are updated)
-  constexpr bool EA = ALG0 == 21 && S::n2 > 0;
-  v4d A22[EA ? S::n2 : 1];
-  auto ea_count = [](int bb) { return (bb + 1) * H - bb * (bb + 1) / 2; };   // blocks retired by row bb
-  // ALG0 24: only A22's first block row (H, H..NB-1), loaded before the last
-  // phase-1 panel, when rows < H - 1 have retired their (bb, j < H) blocks
-  constexpr bool EAL = ALG0 == 24 && S::n2 > 0 && H >= 2;
-  constexpr int EAN = EAL ? NB - H : 1;
-  v4d A22L[EAN];
   static_for<0, H>([&](auto BI) {
     constexpr int bi = decltype(BI)::value;
     static_for<bi, NB>([&](auto BJ) {
       constexpr int bj = decltype(BJ)::value;
-      if constexpr (PRE && bi == 0) {
+      if constexpr (bi == 0) {
         U1[S::i1(0, bj)] = pre[bj];
         if constexpr (bj == 0) {
           const double pd = phinv[c];
@@ -1211,27 +950,12 @@ void chol_mfma_kernel(const CholJob* __restrict__ jobs, int B, long long u0, int
       }
     });
   });
-  // ALG 10 (lookahead): step bb updates only the next row (bb + 1) at once; its
-  // updates of rows >= bb + 2 are spread over the pivots of panel bb + 1
-  // (same blocks, same order per block: bit-identical to ALG 8)
-  constexpr bool LA = ALG == 10;
   static_for<0, H>([&](auto BBc) {
     constexpr int bb = decltype(BBc)::value;
-    auto fill = [&](auto Kc) {
-      if constexpr (LA && bb >= 1) {
-        constexpr int k = decltype(Kc)::value;
-        constexpr int r0 = bb + 1, F = tri_count(NB, r0, H);
-        constexpr int np = (bb == NB - 1) ? 15 : 16;
-        constexpr int t0 = (k * F + np - 1) / np, t1 = ((k + 1) * F + np - 1) / np;
-        static_for<t0, t1>([&](auto T) {
-          constexpr int i = tri_row(NB, r0, decltype(T)::value), j = tri_col(NB, r0, decltype(T)::value);
-          syrk_update(U1[S::i1(i, j)], U1[S::i1(bb - 1, i)], U1[S::i1(bb - 1, j)]);
-        });
-      }
-    };
-    panel(BBc, [&](auto JJ) -> v4d& { return U1[S::i1(bb, decltype(JJ)::value)]; }, fill);
+    panel_ldl_row<NB, ALG, KEEP == 0, PACK1>(BBc, [&](auto JJ) -> v4d& { return U1[S::i1(bb, decltype(JJ)::value)]; },
+                                             q, c, ldet, ok, NoHook{}, klast);
     EWH_STAMP(2 + 2 * bb)
-    static_for<bb + 1, (LA ? (bb + 2 < H ? bb + 2 : H) : H)>([&](auto II) {
+    static_for<bb + 1, H>([&](auto II) {
       constexpr int i = decltype(II)::value;
       static_for<i, NB>([&](auto JJ) {
         constexpr int j = decltype(JJ)::value;
@@ -1239,28 +963,7 @@ void chol_mfma_kernel(const CholJob* __restrict__ jobs, int B, long long u0, int
       });
     });
     EWH_STAMP(3 + 2 * bb)
-    if constexpr (EAL && bb == H - 2) {
-      static_for<0, EAN>([&](auto T) {
-        constexpr int j = H + decltype(T)::value;
-        static_for<0, 4>([&](auto R) {
-          constexpr int r = decltype(R)::value;
-          A22L[decltype(T)::value][r] = A[(long long)(16 * H + q + 4 * r) * LD + 16 * j + c];
-        });
-      });
-    }
-    if constexpr (EA) {
-      constexpr int t0 = bb == 0 ? 0 : ((bb * H - (bb - 1) * bb / 2) < S::n2 ? (bb * H - (bb - 1) * bb / 2) : S::n2);
-      constexpr int t1 = ((bb + 1) * H - bb * (bb + 1) / 2) < S::n2 ? ((bb + 1) * H - bb * (bb + 1) / 2) : S::n2;
-      static_for<t0, (bb == H - 1 ? S::n2 : t1)>([&](auto T) {
-        constexpr int i = tri_row(NB, H, decltype(T)::value), j = tri_col(NB, H, decltype(T)::value);
-        static_for<0, 4>([&](auto R) {
-          constexpr int r = decltype(R)::value;
-          A22[decltype(T)::value][r] = A[(long long)(16 * i + q + 4 * r) * LD + 16 * j + c];
-        });
-      });
-    }
   });
-  (void)ea_count;
   // ---- phase 2: A22 -= U12^T U12 ----
   // block by block in row order: U1 column i is dead once row i of A22 is done
   v4d U2[S::n2];
@@ -1268,27 +971,7 @@ void chol_mfma_kernel(const CholJob* __restrict__ jobs, int B, long long u0, int
     constexpr int i = decltype(II)::value;
     static_for<i, NB>([&](auto JJ) {
       constexpr int j = decltype(JJ)::value;
-      if constexpr (EAL && i == H) {
-        U2[S::i2(i, j)] = A22L[j - H];
-        if constexpr (i == j) {
-          const double pd = phinv[16 * i + c];
-          static_for<0, 4>([&](auto R) {
-            constexpr int r = decltype(R)::value;
-            U2[S::i2(i, j)][r] += (q + 4 * r == c) ? pd : 0.0;
-          });
-        }
-      } else if constexpr (EA) {
-        U2[S::i2(i, j)] = A22[S::i2(i, j)];
-        if constexpr (i == j) {
-          const double pd = phinv[16 * i + c];
-          static_for<0, 4>([&](auto R) {
-            constexpr int r = decltype(R)::value;
-            U2[S::i2(i, j)][r] += (q + 4 * r == c) ? pd : 0.0;
-          });
-        }
-      } else {
-        load_block(II, JJ, U2[S::i2(i, j)]);
-      }
+      load_block(II, JJ, U2[S::i2(i, j)]);
       static_for<0, H>([&](auto BBc) {
         constexpr int bb = decltype(BBc)::value;
         syrk_update(U2[S::i2(i, j)], U1[S::i1(bb, i)], U1[S::i1(bb, j)]);
@@ -1299,22 +982,10 @@ void chol_mfma_kernel(const CholJob* __restrict__ jobs, int B, long long u0, int
   // ---- phase 3: factor A22 (up to the kept blocks) ----
   static_for<H, NB - KEEP>([&](auto BBc) {
     constexpr int bb = decltype(BBc)::value;
-    auto fill = [&](auto Kc) {
-      if constexpr (LA && bb >= H + 1) {
-        constexpr int k = decltype(Kc)::value;
-        constexpr int r0 = bb + 1, F = tri_count(NB, r0, NB);
-        constexpr int np = (bb == NB - 1) ? 15 : 16;
-        constexpr int t0 = (k * F + np - 1) / np, t1 = ((k + 1) * F + np - 1) / np;
-        static_for<t0, t1>([&](auto T) {
-          constexpr int i = tri_row(NB, r0, decltype(T)::value), j = tri_col(NB, r0, decltype(T)::value);
-          syrk_update(U2[S::i2(i, j)], U2[S::i2(bb - 1, i)], U2[S::i2(bb - 1, j)]);
-        });
-      }
-    };
-    panel(BBc, [&](auto JJ) -> v4d& { return U2[S::i2(bb, decltype(JJ)::value)]; }, fill);
+    panel_ldl_row<NB, ALG, KEEP == 0, true>(BBc, [&](auto JJ) -> v4d& { return U2[S::i2(bb, decltype(JJ)::value)]; },
+                                            q, c, ldet, ok, NoHook{}, klast);
     EWH_STAMP(3 + 2 * bb)
-    constexpr bool last = bb == NB - KEEP - 1;
-    static_for<bb + 1, ((LA && !last) ? (bb + 2 < NB ? bb + 2 : NB) : NB)>([&](auto II) {
+    static_for<bb + 1, NB>([&](auto II) {
       constexpr int i = decltype(II)::value;
       static_for<i, NB>([&](auto JJ) {
         constexpr int j = decltype(JJ)::value;
@@ -1345,19 +1016,15 @@ void chol_mfma_kernel(const CholJob* __restrict__ jobs, int B, long long u0, int
       });
     });
   }
-  double ldet_v = ldet.value();
-  bool ok_all = ok;
-  if constexpr (ALG >= 1) {          // per-lane partial log-dets and checks
-    ldet_v = wave_sum(ldet_v);
-    ok_all = __all(ok);
-  }
+  const double ldet_v = wave_sum(ldet.value());    // per-lane partial log-dets (pivots and phi)
+  const bool ok_all = __all(ok);
   if (lane == 0) {
-    double lnl = J.K[(long long)(b - b_off) * J.kstride] - 0.5 * qv - 0.5 * ldet_v - 0.5 * lphi_sum;
+    double lnl = J.K[(long long)(b - b_off) * J.kstride] - 0.5 * qv - 0.5 * ldet_v;
     if (!ok_all || J.fail) lnl = -INFINITY;
     out_units[(long long)p * B + b] = lnl;
   }
 #ifdef EWH_DEV
-  if constexpr (ALG0 == 15 || ALG0 == 20) {
+  if constexpr (STAMP) {
     EWH_STAMP(3 + 2 * NB)
     if (lane == 0 && blockIdx.x < STAMP_UNITS) {
       long long* o = g_stamps + (long long)blockIdx.x * STAMP_N;
@@ -1369,7 +1036,6 @@ void chol_mfma_kernel(const CholJob* __restrict__ jobs, int B, long long u0, int
 #endif
 #undef EWH_STAMP
 }
-
 // ----------------------------------------------------------------------------
 // batched factorisation for wide bases (NB > 9, e.g. C4's 193-wide Sigma):
 // one wave per unit, LEFT-looking over block rows.  Block row i (<= NB
@@ -1398,9 +1064,11 @@ void chol_big_kernel(const CholJob* __restrict__ jobs, int B, long long u0, int 
   const long long u = u0 + xcd_unit(blockIdx.x, gridDim.x);
   const int p = (int)(u / B), b = (int)(u % B);
   const CholJob J = jobs[p];
-  const double* A = J.mats + (long long)(b - b_off) * J.mstride;
+  const gdptr A = (gdptr)(J.mats + (long long)(b - b_off) * J.mstride);
   const double* th = theta + (long long)b * ldth;
-  double* scr = scratch + (long long)blockIdx.x * (NB * (NB + 1) / 2) * 256 + lane * 4;
+  typedef __attribute__((address_space(1))) v4d gv4d;   // global_load / store (see gdptr)
+  __attribute__((address_space(1))) double* scr =
+      (__attribute__((address_space(1))) double*)(scratch + (long long)blockIdx.x * (NB * (NB + 1) / 2) * 256 + lane * 4);
 
   LogAcc lphi;
   for (int a = lane; a < LD; a += 64) {
@@ -1442,20 +1110,20 @@ void chol_big_kernel(const CholJob* __restrict__ jobs, int B, long long u0, int 
       // (the compiler issues the row's loads ahead of its MFMAs)
 #pragma unroll 1
       for (int pp = 0; pp < i; ++pp) {
-        const v4d Ui = *(const v4d*)(scr + big_blk<NB>(pp, i) * 256);
+        const v4d Ui = *(const gv4d*)(scr + big_blk<NB>(pp, i) * 256);
         static_for<0, W>([&](auto JJ) {
           constexpr int jj = decltype(JJ)::value;
-          const v4d Uj = *(const v4d*)(scr + big_blk<NB>(pp, i + jj) * 256);
+          const v4d Uj = *(const gv4d*)(scr + big_blk<NB>(pp, i + jj) * 256);
           syrk_update(R[jj], Ui, Uj);
         });
       }
     }
-    panel_ldl_row<NB, 0, 1>(I, [&](auto JJ) -> v4d& { return R[decltype(JJ)::value - i]; }, q, c, ldet, ok,
-                            nullptr);
+    panel_ldl_row<NB, PANEL_2L, true, true>(I, [&](auto JJ) -> v4d& { return R[decltype(JJ)::value - i]; }, q, c,
+                                            ldet, ok);
     if constexpr (i < NB - 1) {
       static_for<0, W>([&](auto JJ) {
         constexpr int j = i + decltype(JJ)::value;
-        *(v4d*)(scr + big_blk<NB>(i, j) * 256) = R[j - i];
+        *(gv4d*)(scr + big_blk<NB>(i, j) * 256) = R[j - i];
       });
     } else {
       qv = readlane_d(R[0][3], 63);
@@ -1508,7 +1176,8 @@ int launch_partial_nb(int nb, int keep, const CholJob* jobs, int B, long long u0
                       const double* theta, int ldth, double* units, double* keep_out, int keep_bs, hipStream_t st);
 // dynamic-LDS attributes of the contraction kernels on the current device
 int set_contract_attributes();
-// true in the dev library (make dev, -DEWH_DEV): kernel A/B modes 3-6, 8-15 compiled in
-bool ab_variants_built();
+// true when kernel A/B mode `mode` (>= 3, not 7) is compiled into this library
+// (dev library only: make dev, -DEWH_DEV)
+bool variant_built(int mode);
 
 }  // namespace ewh_dev

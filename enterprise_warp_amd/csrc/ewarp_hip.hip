@@ -98,20 +98,58 @@ __global__ __launch_bounds__(256) void epoch_sums_kernel(PsrDev P, const double*
 }
 
 // ----------------------------------------------------------------------------
+// double-double helpers (Knuth TwoSum, TwoProd by fma; Dekker / Bailey
+// normalisation): value = hi + lo with |lo| <= ulp(hi) / 2
+// ----------------------------------------------------------------------------
+struct dd {
+  double hi, lo;
+};
+__device__ __forceinline__ dd dd_two_sum(double a, double b) {
+  const double s = a + b, bp = s - a;
+  return {s, (a - (s - bp)) + (b - bp)};
+}
+__device__ __forceinline__ dd dd_fast(double a, double b) {   // |a| >= |b|
+  const double s = a + b;
+  return {s, b - (s - a)};
+}
+__device__ __forceinline__ dd dd_add(dd x, dd y) {
+  const dd s = dd_two_sum(x.hi, y.hi);
+  return dd_fast(s.hi, s.lo + x.lo + y.lo);
+}
+__device__ __forceinline__ dd dd_mul(dd x, dd y) {
+  const double p = x.hi * y.hi;
+  return dd_fast(p, fma(x.hi, y.hi, -p) + (x.hi * y.lo + x.lo * y.hi));
+}
+__device__ __forceinline__ dd dd_div(dd x, dd y) {          // one Newton correction of x.hi / y.hi
+  const double q = x.hi / y.hi;
+  const dd r = dd_add(x, dd_mul({-q, 0.0}, y));
+  return dd_fast(q, r.hi / y.hi);
+}
+__device__ __forceinline__ dd dd_sqrt(dd x) {
+  const double r = sqrt(x.hi);
+  const dd e = dd_add(x, dd_mul({-r, 0.0}, {r, 0.0}));
+  return dd_fast(r, e.hi / (2.0 * r));
+}
+
+// ----------------------------------------------------------------------------
 // fixed white noise, one-off (ewh_create / ewh_set_fixed_white): the cached
 // Gram G = T_aug^T W T_aug - sum_e beta_e s_e s_e^T with every entry summed
-// in double-double (Dot2, Ogita-Rump-Oishi 2005: TwoProd by fma, TwoSum),
-// as if in twice the working precision.  The MFMA contraction sums an entry
-// over up to 20k TOAs in one fp64 accumulator; prior draws whose Sigma is
-// ill-conditioned after the timing-model elimination amplified that rounding
-// to ~1e-1 in lnL on C3 (tests/test_gpu_parity.py::
+// in double-double (Dot2, Ogita-Rump-Oishi 2005: TwoProd by fma, TwoSum) and
+// kept as hi + lo for the double-double timing-model elimination
+// (schur_kernel).  The products are exact: w T_a is itself split by TwoProd,
+// so each term is w_t T_ta T_tb with only w_t = 1/N_t rounded once (a
+// relative perturbation of N_t by <= 2^-53); the epoch sums s_e are fp64
+// (<= 16-32 TOAs each).  One fp64 MFMA accumulator over 20k TOAs moved
+// prior-draw lnL by up to 7e-2 on C3 through the ill-conditioned
+// timing-model elimination (tests/test_gpu_parity.py::
 // test_c3_bench_workload_prior_draws).  One workgroup per upper 16x16 block,
 // thread (ty, tx) -> entry (16 bi + ty, 16 bj + tx); 32-row TOA chunks staged
 // in LDS.  (Chromatic `vary` bases never take this path: their basis is
 // theta-dependent, so white noise is not cached.)
 __global__ __launch_bounds__(256) void gram_dd_kernel(PsrDev P, const double* __restrict__ w,
                                                       const double* __restrict__ beta,
-                                                      const double* __restrict__ s, double* __restrict__ G) {
+                                                      const double* __restrict__ s, double* __restrict__ G,
+                                                      double* __restrict__ Glo) {
   const int LD = P.ld, nb = P.nb;
   int blk = blockIdx.x, bi = 0;
   while (blk >= nb - bi) { blk -= nb - bi; ++bi; }
@@ -134,43 +172,53 @@ __global__ __launch_bounds__(256) void gram_dd_kernel(PsrDev P, const double* __
       if (threadIdx.x < 32) wv[threadIdx.x] = t0 + (int)threadIdx.x < nrows ? sg * ws[t0 + threadIdx.x] : 0.0;
       __syncthreads();
       for (int r = 0; r < 32; ++r) {
-        const double x = wv[r] * Ta[r][ty], y = Tb[r][tx];
+        const double wa = wv[r], ta = Ta[r][ty], y = Tb[r][tx];
+        const double x = wa * ta;
+        const double xe = fma(wa, ta, -x);          // TwoProd: w T_a = x + xe exactly
         const double p = x * y;
         const double pe = fma(x, y, -p);            // TwoProd: x y = p + pe exactly
         const double sum = hi + p;                  // TwoSum: hi + p = sum + se exactly
         const double bp = sum - hi;
         const double se = (hi - (sum - bp)) + (p - bp);
         hi = sum;
-        lo += se + pe;
+        lo += se + fma(xe, y, pe);
       }
       __syncthreads();
     }
   }
   const int row = 16 * bi + ty, col = 16 * bj + tx;
   if (row > col) return;      // diagonal block: the upper entry's thread writes both (exactly symmetric)
-  double v = hi + lo;
-  if (row == col && row >= P.m && row < LD - 1) v = 1.0;   // unit pads, as the contraction kernels
-  G[(long long)row * LD + col] = v;
-  G[(long long)col * LD + row] = v;
+  dd v = dd_fast(hi, lo);
+  if (row == col && row >= P.m && row < LD - 1) v = {1.0, 0.0};   // unit pads, as the contraction kernels
+  G[(long long)row * LD + col] = v.hi;
+  G[(long long)col * LD + row] = v.hi;
+  Glo[(long long)row * LD + col] = v.lo;
+  Glo[(long long)col * LD + row] = v.lo;
 }
 
 // ----------------------------------------------------------------------------
 // fixed white noise: eliminate the leading constant-phi (timing-model) block
-// of G once; write the reduced matrix S (fx_ld x fx_ld, r last) and K.
-// One 256-thread block per pulsar; G is modified in place.
+// of G = Ghi + Glo once, in double-double (Cholesky, row k scaled by
+// 1/sqrt(pivot)); write the reduced matrix S (fx_ld x fx_ld, r last, rounded
+// to fp64) and K.  The elimination cancels most of the low-frequency Fourier
+// columns' Gram (they are close to the span of the spin-down columns), so it
+// runs on the double-double Gram.  One 256-thread block per
+// pulsar; Ghi / Glo are modified in place.
 // ----------------------------------------------------------------------------
-__global__ __launch_bounds__(256) void schur_kernel(double* G, int ld, int m, int nlead,
+__global__ __launch_bounds__(256) void schur_kernel(double* Ghi, double* Glo, int ld, int m, int nlead,
                                                     const int* __restrict__ col_ptr,
                                                     const DSpec* __restrict__ spec,
                                                     double Kb, double* S, int fx_ld, int nloc, int gstart,
                                                     int ncommon, double* Kout, int* fail_out) {
-  __shared__ double row[256 * 4];
+  __shared__ double rh[256 * 4], rl[256 * 4];
   __shared__ double red[4];
   double lphi = 0.0;
   for (int a = threadIdx.x; a < nlead; a += 256) {
     double ph = 0.0;
     for (int e = col_ptr[a]; e < col_ptr[a + 1]; ++e) ph += spec_phi(spec[e], nullptr);
-    G[(long long)a * ld + a] += 1.0 / ph;
+    const dd v = dd_add({Ghi[(long long)a * ld + a], Glo[(long long)a * ld + a]}, {1.0 / ph, 0.0});
+    Ghi[(long long)a * ld + a] = v.hi;
+    Glo[(long long)a * ld + a] = v.lo;
     lphi += log(ph);
   }
   lphi = block_sum256(lphi, red);
@@ -178,16 +226,24 @@ __global__ __launch_bounds__(256) void schur_kernel(double* G, int ld, int m, in
   double logdet = 0.0;
   int ok = 1;
   for (int k = 0; k < nlead; ++k) {
-    const double piv = G[(long long)k * ld + k];
-    ok &= piv > 0.0;
-    const double d = sqrt(piv), rinv = 1.0 / d;
-    logdet += log(d);
+    const dd piv = {Ghi[(long long)k * ld + k], Glo[(long long)k * ld + k]};
+    ok &= piv.hi > 0.0;
+    const dd d = dd_sqrt(piv);
+    logdet += log(d.hi) + d.lo / d.hi;
     __syncthreads();
-    for (int j = k + 1 + threadIdx.x; j < ld; j += 256) row[j] = G[(long long)k * ld + j] * rinv;
+    for (int j = k + 1 + threadIdx.x; j < ld; j += 256) {
+      const dd x = dd_div({Ghi[(long long)k * ld + j], Glo[(long long)k * ld + j]}, d);
+      rh[j] = x.hi;
+      rl[j] = x.lo;
+    }
     __syncthreads();
     for (int i = k + 1; i < ld; ++i) {
-      const double ri = row[i];
-      for (int j = k + 1 + threadIdx.x; j < ld; j += 256) G[(long long)i * ld + j] -= ri * row[j];
+      const dd ri = {rh[i], rl[i]};
+      for (int j = k + 1 + threadIdx.x; j < ld; j += 256) {
+        const dd v = dd_add({Ghi[(long long)i * ld + j], Glo[(long long)i * ld + j]}, dd_mul({-ri.hi, -ri.lo}, {rh[j], rl[j]}));
+        Ghi[(long long)i * ld + j] = v.hi;
+        Glo[(long long)i * ld + j] = v.lo;
+      }
     }
     __syncthreads();
   }
@@ -205,7 +261,7 @@ __global__ __launch_bounds__(256) void schur_kernel(double* G, int ld, int m, in
     const int gb = gmap(bcol);
     double v;
     if (ga < 0 || gb < 0) v = (a == bcol) ? 1.0 : 0.0;
-    else v = G[(long long)ga * ld + gb];
+    else v = Ghi[(long long)ga * ld + gb] + Glo[(long long)ga * ld + gb];
     S[idx] = v;
   }
   if (threadIdx.x == 0) {
@@ -560,7 +616,7 @@ __global__ __launch_bounds__(256) void dchol_diag_kernel(double* __restrict__ ma
 constexpr int DW_SLOTS = 14;
 __host__ __device__ constexpr int dw_u(int s, int t) { return 8 + (s == 0 ? t - 1 : s == 1 ? t + 1 : 5); }
 
-struct DiagHook : NoFill {
+struct DiagHook : NoHook {
   double* W;
   int bb;
   __device__ __forceinline__ void on_e(const v4d& E) const { *(v4d*)(W + bb * 256) = E; }
@@ -598,8 +654,8 @@ __global__ __launch_bounds__(64) void dchol_diag_reg_kernel(double* __restrict__
     DiagHook hk;
     hk.W = W;
     hk.bb = bb;
-    panel_ldl_row<4, 1, 7, LAST>(BBc, [&](auto JJ) -> v4d& { return U[id(bb, decltype(JJ)::value)]; }, q, c, ld, ok,
-                                 nullptr, hk);
+    panel_ldl_row<4, PANEL_2L, LAST, false>(BBc, [&](auto JJ) -> v4d& { return U[id(bb, decltype(JJ)::value)]; }, q,
+                                            c, ld, ok, hk);
     static_for<bb + 1, 4>([&](auto II) {
       constexpr int i = decltype(II)::value;
       static_for<i, 4>([&](auto JJ) {
@@ -1451,9 +1507,9 @@ int setup_fixed(DevCtx* h) {
     maxld = std::max(maxld, (size_t)ps.ld);
   }
   TmpBufs tmp;
-  double *w, *beta, *s, *G, *Kb, *dummy_theta;
+  double *w, *beta, *s, *G, *Glo, *Kb, *dummy_theta;
   if ((rc = tmp.get(&w, maxn)) || (rc = tmp.get(&beta, maxe)) || (rc = tmp.get(&s, maxe * maxld)) ||
-      (rc = tmp.get(&G, maxld * maxld)) || (rc = tmp.get(&Kb, 1)) ||
+      (rc = tmp.get(&G, maxld * maxld)) || (rc = tmp.get(&Glo, maxld * maxld)) || (rc = tmp.get(&Kb, 1)) ||
       (rc = tmp.get(&dummy_theta, std::max(1, h->n_param))))
     return rc;
   // theta is never read (every white-noise slot is constant)
@@ -1469,16 +1525,18 @@ int setup_fixed(DevCtx* h) {
     if (ps.n_epoch > 0)
       hipLaunchKernelGGL(epoch_sums_kernel, dim3(ps.n_epoch, 1), dim3(256), 0, h->stream, ps.dev, w, nullptr, s);
     if (ps.dev.n_bgroup == 0 && h->kernel_mode != 7) {
-      hipLaunchKernelGGL(gram_dd_kernel, dim3(ps.nb * (ps.nb + 1) / 2), dim3(256), 0, h->stream, ps.dev, w, beta, s, G);
+      hipLaunchKernelGGL(gram_dd_kernel, dim3(ps.nb * (ps.nb + 1) / 2), dim3(256), 0, h->stream, ps.dev, w, beta, s, G,
+                         Glo);
       EWH_HIP(hipGetLastError());
-    } else if ((rc = launch_contract_nb(ps.nb, ps.dev, w, beta, s, nullptr, G, 1, h->stream))) {
-      return rc;
+    } else {
+      EWH_HIP(hipMemsetAsync(Glo, 0, sizeof(double) * (size_t)ps.ld * ps.ld, h->stream));
+      if ((rc = launch_contract_nb(ps.nb, ps.dev, w, beta, s, nullptr, G, 1, h->stream))) return rc;
     }
     double Kb_h = 0.0;
     EWH_HIP(hipMemcpyAsync(&Kb_h, Kb, sizeof(double), hipMemcpyDeviceToHost, h->stream));
     EWH_HIP(hipStreamSynchronize(h->stream));
     if (!ps.d_S && (rc = dalloc(h, &ps.d_S, (size_t)ps.fx_ld * ps.fx_ld))) return rc;
-    hipLaunchKernelGGL(schur_kernel, dim3(1), dim3(256), 0, h->stream, G, ps.ld, ps.m, ps.nlead, ps.d_colptr,
+    hipLaunchKernelGGL(schur_kernel, dim3(1), dim3(256), 0, h->stream, G, Glo, ps.ld, ps.m, ps.nlead, ps.d_colptr,
                        ps.d_spec, Kb_h, ps.d_S, ps.fx_ld, ps.nloc, ps.gstart, ps.ncommon, h->d_fxK + p,
                        h->d_fxfail + p);
     EWH_HIP(hipGetLastError());
@@ -1712,8 +1770,108 @@ void destroy_ctx(DevCtx* h) {
   delete h;
 }
 
+// Timing-model projection of one pulsar's basis.  Every
+// basis column that does not depend on theta, and the residual, loses its
+// least-squares component along the leading constant-phi (timing-model)
+// columns M under the weights 1/sigma^2:
+//   X' = X - M C,   C = (M^T W0 M)^-1 M^T W0 X.
+// With phi_M = 1e40 this is an exact reparametrisation of the same
+// likelihood: the timing-model coefficients absorb M C b (prior ~ flat), so
+// lnL, log|Sigma| and the quadratic form change by O(|C|^2 / phi_M) ~ 1e-36
+// relative, and log|phi| is untouched (the map is unit triangular).  What it
+// removes is the cancellation: the low-frequency Fourier columns lie close
+// to the span of the spin-down / astrometric columns, so in the original
+// basis the timing-model elimination subtracts two nearly equal Gram blocks
+// (~1e14 each) and fp64 rounding of the Gram -- or an asymmetric panel --
+// was amplified into the prior-draw lnL (tests/golden, c2_small: 7e5x the
+// strict bound).  C needs no special accuracy: any C is an exact
+// reparametrisation; only X' = X - M C is rounded (once, by fma), a
+// perturbation of X of O(eps |X|) -- the size of X's own representation.
+// Computed once per handle (ProjCoef), applied when T_aug is built.
+struct ProjCoef {
+  int nl = 0;
+  std::vector<int> cols;     // projected basis columns (the residual is cols.size()-th)
+  std::vector<double> C;     // nl x (cols.size() + 1), row-major
+};
+
+ProjCoef projection_coef(const ewh_pulsar_desc& s) {
+  ProjCoef pc;
+  const int nl = s.n_lead_const, n = s.n_toa;
+  if (nl <= 0 || nl >= s.n_col + 1) return pc;
+  for (int j = nl; j < s.n_col; ++j)
+    if (s.n_bgroup == 0 || s.col_bgroup[j] < 0) pc.cols.push_back(j);
+  const int nc = (int)pc.cols.size() + 1;
+  std::vector<double> G0((size_t)nl * nl, 0.0), Bm((size_t)nl * nc, 0.0), x(nc);
+  for (int t = 0; t < n; ++t) {
+    const double* row = s.basis + (size_t)t * s.n_col;
+    const double w0 = 1.0 / (s.toaerr[t] * s.toaerr[t]);
+    for (int k = 0; k < nc - 1; ++k) x[k] = row[pc.cols[k]];
+    x[nc - 1] = s.resid[t];
+    for (int a = 0; a < nl; ++a) {
+      const double wa = w0 * row[a];
+      if (wa == 0.0) continue;
+      for (int b = 0; b < nl; ++b) G0[(size_t)a * nl + b] += wa * row[b];
+      double* br = &Bm[(size_t)a * nc];
+      for (int k = 0; k < nc; ++k) br[k] += wa * x[k];
+    }
+  }
+  // Cholesky of G0; a column of M with (numerically) no weight of its own --
+  // e.g. a zero-norm design-matrix column -- is left out of the projection
+  double dmax = 0.0;
+  for (int a = 0; a < nl; ++a) dmax = std::max(dmax, G0[(size_t)a * nl + a]);
+  std::vector<double> L((size_t)nl * nl, 0.0);
+  std::vector<char> use(nl, 0);
+  for (int k = 0; k < nl; ++k) {
+    double v = G0[(size_t)k * nl + k];
+    for (int j = 0; j < k; ++j) v -= L[(size_t)k * nl + j] * L[(size_t)k * nl + j];
+    if (!(v > 1e-12 * dmax)) continue;
+    use[k] = 1;
+    const double lkk = std::sqrt(v);
+    L[(size_t)k * nl + k] = lkk;
+    for (int i = k + 1; i < nl; ++i) {
+      double u = G0[(size_t)i * nl + k];
+      for (int j = 0; j < k; ++j) u -= L[(size_t)i * nl + j] * L[(size_t)k * nl + j];
+      L[(size_t)i * nl + k] = u / lkk;
+    }
+  }
+  // C = G0^-1 Bm over the used columns (forward, then back substitution)
+  pc.nl = nl;
+  pc.C.assign((size_t)nl * nc, 0.0);
+  for (int k = 0; k < nc; ++k) {
+    std::vector<double> y(nl, 0.0);
+    for (int i = 0; i < nl; ++i) {
+      if (!use[i]) continue;
+      double v = Bm[(size_t)i * nc + k];
+      for (int j = 0; j < i; ++j) v -= L[(size_t)i * nl + j] * y[j];
+      y[i] = v / L[(size_t)i * nl + i];
+    }
+    for (int i = nl - 1; i >= 0; --i) {
+      if (!use[i]) continue;
+      double v = y[i];
+      for (int j = i + 1; j < nl; ++j) v -= L[(size_t)j * nl + i] * pc.C[(size_t)j * nc + k];
+      pc.C[(size_t)i * nc + k] = v / L[(size_t)i * nl + i];
+    }
+  }
+  return pc;
+}
+
+// X' = X - M C on T_aug (row-major, leading dimension ld, residual at ld-1)
+void apply_projection(const ProjCoef& pc, int n_toa, int ld, std::vector<double>& Ta) {
+  const int nl = pc.nl, nc = (int)pc.cols.size() + 1;
+  if (nl == 0) return;
+  for (int t = 0; t < n_toa; ++t) {
+    double* row = &Ta[(size_t)t * ld];
+    for (int k = 0; k < nc; ++k) {
+      const int col = k < nc - 1 ? pc.cols[k] : ld - 1;
+      double v = row[col];
+      for (int a = 0; a < nl; ++a) v = std::fma(-row[a], pc.C[(size_t)a * nc + k], v);
+      row[col] = v;
+    }
+  }
+}
+
 // One device's copy of the PTA (every table, the fixed-WN cache, scratch).
-int create_ctx(const ewh_pta_desc* d, int device, DevCtx** out) {
+int create_ctx(const ewh_pta_desc* d, const std::vector<ProjCoef>& proj, int device, DevCtx** out) {
   *out = nullptr;
   int rc;
   EWH_HIP(hipSetDevice(device));
@@ -1764,6 +1922,7 @@ int create_ctx(const ewh_pta_desc* d, int device, DevCtx** out) {
       Ta[(size_t)t * ps.ld + ps.ld - 1] = s.resid[t];
       sig2[t] = s.toaerr[t] * s.toaerr[t];
     }
+    apply_projection(proj[p], s.n_toa, ps.ld, Ta);
     double* dT;
     double* dsig2;
     int *d_ef, *d_eq, *d_es, *d_ee, *d_eslot;
@@ -2199,9 +2358,11 @@ int ewh_create(const ewh_pta_desc* d, const int32_t* device_ids, int32_t ndev, e
   ewh_handle* H = new ewh_handle();
   H->P = d->n_pulsar;
   H->n_param = d->n_param;
+  std::vector<ProjCoef> proj(d->n_pulsar);
+  for (int p = 0; p < d->n_pulsar; ++p) proj[p] = projection_coef(d->pulsars[p]);
   for (int id : ids) {
     DevCtx* c = nullptr;
-    if ((rc = create_ctx(d, id, &c))) {
+    if ((rc = create_ctx(d, proj, id, &c))) {
       ewh_destroy(H);
       return rc;
     }
@@ -2239,8 +2400,9 @@ int ewh_set_fixed_white(ewh_handle* H, const double* values) {
 
 int ewh_set_kernel_mode(ewh_handle* H, int32_t mode) {
   if (!H || mode < 0 || mode > 30) return set_err(EWH_E_INVALID, "bad handle / mode");
-  if (mode >= 3 && mode != 7 && !ab_variants_built())
-    return set_err(EWH_E_UNSUPPORTED, "kernel A/B variants are built only into the dev library (make dev)");
+  if (mode != 0 && mode != 1 && mode != 7 && !variant_built(mode))
+    return set_err(EWH_E_UNSUPPORTED, "kernel mode " + std::to_string(mode) +
+                                          " is not built into this library (A/B variants: the dev library, make dev)");
   for (DevCtx* h : H->ctx) {
     h->kernel_mode = mode;
     (void)hipSetDevice(h->device);

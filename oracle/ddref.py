@@ -1,0 +1,234 @@
+"""TEST INFRASTRUCTURE ONLY — a double-double (~106-bit) reference value of
+the enterprise lnL for uncorrelated / CURN models.
+
+Why: on ill-conditioned prior draws the lnL of the fp64 inputs is so
+sensitive that even the x87 extended-precision restatement
+(device_order_ref with np.longdouble, eps 1.1e-19) carries errors of up to
+~1e2 x the strict bound (tests/golden c2_small sample 1: its plain
+extended-precision Gram summation against an error-free one).  The parity
+criterion "GPU error <= enterprise-order error" (tests/conftest.py
+`check_accuracy`) needs a reference whose own error is far below both.
+
+Arithmetic: numpy arrays of (hi, lo) pairs with Dekker / Knuth error-free
+transformations.  The Gram is error free (device_order_ref.exact_product on
+18-bit slices, summed in double-double); N, the ECORR terms and the spectra
+phi are formed in double-double from the fp64 parameters (powers of ten and
+the power laws through mpmath at 40 digits); the timing-model columns and
+everything else are factored together, as enterprise does, by an unblocked
+double-double Cholesky; log d_k = log(hi) + lo/hi.
+"""
+import mpmath
+import numpy as np
+
+from .device_order_ref import TM_PHI, _SPLIT, _slices, two_prod
+from .enterprise_ref import FYR, OraclePTA
+
+mpmath.mp.dps = 40
+
+
+# ---- double-double primitives on numpy arrays ------------------------------
+def two_sum(a, b):
+    s = a + b
+    bb = s - a
+    return s, (a - (s - bb)) + (b - bb)
+
+
+def quick(a, b):
+    s = a + b
+    return s, b - (s - a)
+
+
+def dd_add(x, y):
+    s, e = two_sum(x[0], y[0])
+    t, f = two_sum(x[1], y[1])
+    e = e + t
+    s, e = quick(s, e)
+    e = e + f
+    return quick(s, e)
+
+
+def dd_neg(x):
+    return -x[0], -x[1]
+
+
+def dd_mul(x, y):
+    p, e = two_prod(x[0], y[0])
+    e = e + (x[0] * y[1] + x[1] * y[0])
+    return quick(p, e)
+
+
+def dd_div(x, y):
+    q1 = x[0] / y[0]
+    r = dd_add(x, dd_neg(dd_mul((q1, np.zeros_like(q1)), y)))
+    q2 = r[0] / y[0]
+    r = dd_add(r, dd_neg(dd_mul((q2, np.zeros_like(q2)), y)))
+    q3 = r[0] / y[0]
+    return dd_add(quick(q1, q2), (q3, np.zeros_like(q3)))
+
+
+def dd_log(x):
+    """log of a positive double-double to ~1e-16 absolute (enough for a log-det)."""
+    return np.log(x[0]) + x[1] / x[0]
+
+
+def dd_from_mp(v):
+    hi = float(v)
+    return hi, float(v - mpmath.mpf(hi))
+
+
+def dd_of(a):
+    a = np.asarray(a, float)
+    return a, np.zeros_like(a)
+
+
+# ---- model pieces -----------------------------------------------------------
+def dd_gram(X, w):
+    """G = X^T diag(w) X with w a double-double vector: X w_hi = A_hi + A_lo
+    exactly (TwoProduct), A_hi^T X error free (18-bit slices: exact fp64
+    products and sums, combined in double-double), the remainder
+    (A_lo + X w_lo)^T X by one fp64 product (a 2^-106-relative term)."""
+    A_hi, A_lo = two_prod(X, w[0][:, None])
+    A_lo = A_lo + X * w[1][:, None]
+    SA, SB = _slices(A_hi), _slices(X)
+    k = len(SA)
+    acc = (np.zeros((X.shape[1], X.shape[1])), np.zeros((X.shape[1], X.shape[1])))
+    for s in range(k):
+        for t in range(k - s):
+            acc = dd_add(acc, dd_of(SA[s].T @ SB[t]))
+    return dd_add(acc, dd_of(A_lo.T @ X))
+
+
+def pow10_dd(x):
+    return dd_from_mp(mpmath.power(10, 2 * mpmath.mpf(float(x))))
+
+
+def spectrum_dd(g, p):
+    """phi of one GP signal on its columns (enterprise_ref.powerlaw /
+    powerlaw_bpl / free_spectrum) in double-double via mpmath."""
+    f = np.asarray(g["f"], float)
+    comp = g["components"]
+    val = lambda ref: float(ref[1]) if ref[0] == "const" else float(p[ref[1]])  # noqa: E731
+    nm = g["names"]
+    fu = f[::comp]
+    df = np.diff(np.concatenate(([0.0], fu)))
+    pi2 = mpmath.pi ** 2
+    fyr = mpmath.mpf(FYR)
+    out = []
+    for j in range(len(fu)):
+        fj, dfj = mpmath.mpf(float(fu[j])), mpmath.mpf(float(df[j]))
+        if g["spectrum"] == "powerlaw":
+            A, gam = mpmath.mpf(val(nm["log10_A"])), mpmath.mpf(val(nm["gamma"]))
+            v = mpmath.power(10, 2 * A) / 12 / pi2 * mpmath.power(fyr, gam - 3) * mpmath.power(fj, -gam) * dfj
+        elif g["spectrum"] == "turnover":
+            A, gam, fc = (mpmath.mpf(val(nm["log10_A"])), mpmath.mpf(val(nm["gamma"])), mpmath.mpf(val(nm["fc"])))
+            if fc < 0:
+                fc = mpmath.power(10, fc)
+            v = mpmath.power(10, 2 * A) / 12 / pi2 * mpmath.power(fyr, -3) * mpmath.power((fj + fc) / fyr, -gam) * dfj
+        else:
+            rho = np.asarray(p[nm["log10_rho"][1]] if nm["log10_rho"][0] != "const" else nm["log10_rho"][1], float)
+            v = mpmath.power(10, 2 * mpmath.mpf(float(rho[j])))
+        out.extend([v] * comp)
+    return out
+
+
+class DDReferencePTA:
+    """lnL in double-double for an uncorrelated / CURN model (fixed or varying
+    white noise): per pulsar the full Sigma = TNT + diag(1/phi) (timing model
+    included, phi_tm = 1e40) factored by an unblocked double-double Cholesky
+    with r appended as the last column (its last pivot is
+    q = rNr - d^T Sigma^-1 d)."""
+
+    def __init__(self, psrs, terms_per_psr):
+        self.o = OraclePTA(psrs, terms_per_psr, fixed_params=None)
+        if self.o.correlated():
+            raise ValueError("DDReferencePTA: uncorrelated / CURN models only")
+        self.pulsars = self.o.pulsars
+
+    def _white(self, pp, p):
+        """N diagonal (double-double) and the ECORR epochs (slice, J)."""
+        n = len(pp.r)
+        sig = np.asarray(pp.sigma, float)
+        s2 = two_prod(sig, sig)
+        D = (np.zeros(n), np.zeros(n))
+        for k, masks, names in pp.white:
+            for key, m in masks.items():
+                if k == "efac":
+                    ef = float(p[names[key]])
+                    e2 = two_prod(np.float64(ef), np.float64(ef))
+                    t = dd_mul((np.full(m.sum(), e2[0]), np.full(m.sum(), e2[1])), (s2[0][m], s2[1][m]))
+                elif k == "tnequad":
+                    q = pow10_dd(p[names[key]])
+                    t = (np.full(m.sum(), q[0]), np.full(m.sum(), q[1]))
+                else:
+                    continue
+                Dm = dd_add((D[0][m], D[1][m]), t)
+                D[0][m], D[1][m] = Dm
+        return D, [(slc, pow10_dd(p[nm])) for slc, nm in pp.ecorr]
+
+    def _phi(self, pp, p):
+        m = pp.T.shape[1]
+        phi = [mpmath.mpf(0)] * m
+        for g in pp.gps:
+            if g["kind"] == "tm":
+                for j in g["idx"]:
+                    phi[j] += mpmath.mpf(TM_PHI)
+                continue
+            vals = spectrum_dd(g, p)
+            for j, v in zip(g["idx"], vals):
+                phi[j] += v
+        inv = [dd_from_mp(1 / v) for v in phi]
+        return (np.array([a for a, _ in inv]), np.array([b for _, b in inv])), float(sum(mpmath.log(v) for v in phi))
+
+    def pulsar_terms(self, pp, p):
+        T = np.asarray(pp.basis({k: float(v) for k, v in p.items() if np.ndim(v) == 0}), float)
+        X = np.concatenate([T, np.asarray(pp.r, float)[:, None]], axis=1)
+        m1 = X.shape[1]
+        D, ep = self._white(pp, p)
+        one = (np.ones_like(D[0]), np.zeros_like(D[0]))
+        w = dd_div(one, D)
+        G = dd_gram(X, w)
+        ldn = float(np.sum(dd_log(D)))
+        for slc, J in ep:
+            wi = (w[0][slc], w[1][slc])
+            sw = (np.float64(0.0), np.float64(0.0))
+            for t in range(len(wi[0])):
+                sw = dd_add(sw, (wi[0][t], wi[1][t]))
+            Jd = (np.float64(J[0]), np.float64(J[1]))
+            beta = dd_div((np.float64(1.0), np.float64(0.0)), dd_add(sw, dd_div((np.float64(1.0), np.float64(0.0)), Jd)))
+            sv = (np.zeros(m1), np.zeros(m1))
+            Xs = X[slc]
+            for t in range(Xs.shape[0]):
+                sv = dd_add(sv, dd_mul((Xs[t], np.zeros(m1)), (np.full(m1, wi[0][t]), np.full(m1, wi[1][t]))))
+            outer = dd_mul((sv[0][:, None] * np.ones(m1)[None, :], sv[1][:, None] * np.ones(m1)[None, :]),
+                           (sv[0][None, :] * np.ones(m1)[:, None], sv[1][None, :] * np.ones(m1)[:, None]))
+            G = dd_add(G, dd_neg(dd_mul(outer, (np.full((m1, m1), beta[0]), np.full((m1, m1), beta[1])))))
+            ldn += float(dd_log(Jd) - dd_log(beta))
+        phiinv, lphi = self._phi(pp, p)
+        Gh, Gl = G[0].copy(), G[1].copy()
+        idx = np.arange(m1 - 1)
+        dg = dd_add((Gh[idx, idx], Gl[idx, idx]), phiinv)
+        Gh[idx, idx], Gl[idx, idx] = dg
+        ldet = 0.0
+        for k in range(m1 - 1):
+            d = (Gh[k, k], Gl[k, k])
+            if not d[0] > 0:
+                return -np.inf
+            ldet += float(dd_log(d))
+            u = (Gh[k, k + 1:].copy(), Gl[k, k + 1:].copy())
+            wv = dd_div(u, (np.full(len(u[0]), d[0]), np.full(len(u[0]), d[1])))
+            nn = len(u[0])
+            upd = dd_mul((np.repeat(u[0][:, None], nn, 1), np.repeat(u[1][:, None], nn, 1)),
+                         (np.repeat(wv[0][None, :], nn, 0), np.repeat(wv[1][None, :], nn, 0)))
+            sub = dd_add((Gh[k + 1:, k + 1:], Gl[k + 1:, k + 1:]), dd_neg(upd))
+            Gh[k + 1:, k + 1:], Gl[k + 1:, k + 1:] = sub
+        q = Gh[-1, -1] + Gl[-1, -1]
+        return -0.5 * ldn - 0.5 * q - 0.5 * ldet - 0.5 * lphi
+
+    def lnlikelihood(self, params):
+        tot = 0.0
+        for pp in self.pulsars:
+            v = self.pulsar_terms(pp, params)
+            if not np.isfinite(v):
+                return -np.inf
+            tot += v
+        return float(tot)

@@ -1,6 +1,7 @@
 """Phase timing of the C3 Cholesky kernel from in-kernel s_memtime stamps
-(dev library, kernel mode 21 = the fused-DPP panel with stamps at every
-panel / trailing-update boundary of the first 4096 units).
+(dev library, kernel mode 21 = the default two-level panel with stamps at
+every panel / trailing-update boundary of the first 4096 units; phase split
+H = 3 block rows for NB = 8).
 
     python scripts/chol_stamps.py [--B 4096]
 
@@ -26,7 +27,8 @@ UNITS, NST = 4096, 24
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--B", type=int, default=4096)
-    ap.add_argument("--mode", type=int, default=26)
+    ap.add_argument("--mode", type=int, default=21)
+    ap.add_argument("--H", type=int, default=3)
     args = ap.parse_args()
     import torch
     from enterprise_warp_amd import _lib, synth
@@ -59,10 +61,10 @@ def main():
     t = st[:, :nstamp].astype(np.float64)
     d = np.diff(t, axis=1)
     names = ["phi prologue"]
-    for bb in range(nb // 2):
+    for bb in range(args.H):
         names += [f"panel {bb}", f"trailing {bb}"]
     names += ["phase-2 A22 update"]
-    for bb in range(nb // 2, nb):
+    for bb in range(args.H, nb):
         names += [f"panel {bb}", f"trailing {bb}"]
     names += ["epilogue"]
     names = names[: d.shape[1]]

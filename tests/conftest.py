@@ -12,25 +12,26 @@ sys.path.insert(0, ROOT)
 
 # Parity tolerance of the north star (BASELINE.json): 1e-6 absolute / 1e-10
 # relative in lnL ("strict").  Near-truth samples (where samplers spend their
-# time) are held to strict.  On prior draws the golden fixtures carry a
-# MEASURED per-sample spread: the largest pairwise difference between the
-# enterprise-order oracle, the device-order fp64 restatement and the device-
-# order extended-precision value (oracle/device_order_ref.py,
-# tests/golden/make_golden.py).  Two correct fp64 orderings of the same
-# likelihood really are that far apart there, so such samples are held to
-# max(strict, SPREAD_K * spread).  DESIGN.md §2.
+# time) and full-size checks are held to strict against the enterprise-order
+# oracle.  Prior draws are often so ill-conditioned that the lnL of the fp64
+# inputs is not determined to 1e-10 by ANY fp64 ordering (enterprise's own
+# LAPACK order misses the exact value by up to 6e5 x strict on
+# tests/golden/c2_small); there the GPU is held to ACCURACY: its error
+# against a near-exact reference (oracle/ddref.py double-double, or the
+# extended-precision, error-free-Gram restatement) must not exceed
+# enterprise's own error against it, or strict if that is larger
+# (`check_accuracy`).  Independent of the device's own order.
 ATOL, RTOL = 1e-6, 1e-10
-SPREAD_K = 4.0
 
 
 def pytest_configure(config):
     config.addinivalue_line("markers", "gpu: needs an MI355X (HIP device) and libewarp_hip.so")
-    config.addinivalue_line("markers", "gpu_ab: kernel A/B variants (dev library libewarp_hip_ab.so, "
-                                       "`make -C enterprise_warp_amd/csrc ab`); not part of the driver's -m gpu suite")
+    config.addinivalue_line("markers", "gpu_ab: kernel A/B variants (dev library libewarp_hip_dev.so, "
+                                       "`make -C enterprise_warp_amd/csrc dev`); not part of the driver's -m gpu suite")
 
 
 def pytest_collection_modifyitems(config, items):
-    skip = pytest.mark.skip(reason="A/B variant tests need a GPU and the dev library (make ab)")
+    skip = pytest.mark.skip(reason="A/B variant tests need a GPU and the dev library (make dev)")
     for it in items:
         if "gpu_ab" in it.keywords and not gpu_available():
             it.add_marker(skip)
@@ -40,20 +41,7 @@ def strict_tolerance(ref):
     return ATOL + RTOL * np.abs(np.asarray(ref, dtype=float))
 
 
-def lnl_tolerance(ref, spread=None, near=None):
-    """strict; or max(strict, SPREAD_K * spread) on samples that are not
-    near-truth (`near` False) when a measured spread is given."""
-    tol = strict_tolerance(ref)
-    if spread is not None:
-        wide = np.maximum(tol, SPREAD_K * np.asarray(spread, dtype=float))
-        tol = wide if near is None else np.where(np.asarray(near, bool), tol, wide)
-    return tol
-
-
-def check_parity(got, want, label, spread=None, near=None):
-    """GPU lnL vs a reference: no NaN, every non-finite value exactly -inf and
-    exactly where the reference is -inf, finite values within lnl_tolerance.
-    Prints max err / strict tolerance.  Returns that ratio."""
+def _finite_pattern(got, want, label):
     got = np.asarray(got, dtype=float)
     want = np.asarray(want, dtype=float)
     assert not np.isnan(got).any(), f"{label}: NaN in GPU lnL at {np.flatnonzero(np.isnan(got))}"
@@ -62,18 +50,54 @@ def check_parity(got, want, label, spread=None, near=None):
     fin_g, fin_w = np.isfinite(got), np.isfinite(want)
     assert np.array_equal(fin_g, fin_w), \
         f"{label}: -inf pattern differs (gpu -inf at {np.flatnonzero(~fin_g)}, ref -inf at {np.flatnonzero(~fin_w)})"
-    if not fin_w.any():
+    return got, want, fin_w
+
+
+def check_parity(got, want, label):
+    """GPU lnL vs a reference at the strict bound: no NaN, every non-finite
+    value exactly -inf and exactly where the reference is -inf, finite values
+    within 1e-6 + 1e-10 |lnL|.  Prints and returns max err / strict."""
+    got, want, fin = _finite_pattern(got, want, label)
+    if not fin.any():
         return 0.0
-    err = np.abs(got[fin_w] - want[fin_w])
-    tol = lnl_tolerance(want[fin_w], None if spread is None else np.asarray(spread)[fin_w],
-                        None if near is None else np.asarray(near)[fin_w])
-    ratio = err / strict_tolerance(want[fin_w])
-    print(f"{label}: max err/strict {ratio.max():.3e}, max err/tol {np.max(err / tol):.3e} over {fin_w.sum()} samples")
-    ok = err <= tol
-    k = int(np.argmax(err / tol))
-    assert ok.all(), f"{label}: {(~ok).sum()} samples outside tolerance; worst sample {np.flatnonzero(fin_w)[k]}: " \
-                     f"err {err[k]:.3e} > tol {tol[k]:.3e}"
+    ratio = np.abs(got[fin] - want[fin]) / strict_tolerance(want[fin])
+    print(f"{label}: max err/strict {ratio.max():.3e} over {fin.sum()} samples")
+    k = int(np.argmax(ratio))
+    assert ratio.max() <= 1.0, f"{label}: {(ratio > 1).sum()} samples outside strict; worst sample " \
+                               f"{np.flatnonzero(fin)[k]}: err/strict {ratio[k]:.3e}"
     return float(ratio.max())
+
+
+def check_accuracy(got, ent, ext, label, near=None):
+    """The parity criterion on prior draws: per sample |gpu - ext| <=
+    max(|ent - ext|, strict) -- the GPU no less accurate than enterprise's
+    own order against the near-exact value ext -- and on near-truth samples
+    (near True) strict against both.  The -inf pattern must equal the
+    references' exactly; NaN fails.  Returns max over samples of
+    |gpu - ext| / max(|ent - ext|, strict)."""
+    got, ext, fin = _finite_pattern(got, ext, label + " vs extended")
+    ent = np.asarray(ent, dtype=float)
+    assert np.array_equal(np.isfinite(ent), fin), f"{label}: the references disagree on -inf"
+    if not fin.any():
+        return 0.0
+    st = strict_tolerance(ext[fin])
+    eg = np.abs(got[fin] - ext[fin])
+    ee = np.abs(ent[fin] - ext[fin])
+    allow = np.maximum(ee, st)
+    if near is not None:
+        nr = np.asarray(near, bool)[fin]
+        allow = np.where(nr, st, allow)
+        en = np.abs(got[fin] - ent[fin])[nr]
+        if nr.any():
+            assert np.all(en <= strict_tolerance(ent[fin][nr])), \
+                f"{label}: near-truth samples outside strict vs enterprise-order: {en / strict_tolerance(ent[fin][nr])}"
+    r = eg / allow
+    print(f"{label}: |gpu-ext|/strict max {np.max(eg / st):.3e}, |ent-ext|/strict max {np.max(ee / st):.3e}, "
+          f"max |gpu-ext| / max(|ent-ext|, strict) = {r.max():.3f} over {fin.sum()} samples")
+    k = int(np.argmax(r))
+    assert r.max() <= 1.0, f"{label}: sample {np.flatnonzero(fin)[k]}: GPU error {eg[k]:.3e} exceeds " \
+                           f"max(enterprise error {ee[k]:.3e}, strict {st[k]:.3e})"
+    return float(r.max())
 
 
 def oracle_lnl(pta, X):
@@ -90,38 +114,35 @@ def oracle_lnl(pta, X):
     return np.array(out)
 
 
-def orderings_lnl(pta, X):
-    """lnL of every row of X in four correct orderings (enterprise's; the
-    device's factorisation order with a BLAS Gram; reverse-TOA Gram +
-    unblocked Cholesky; the device's order in extended precision) and the
-    measured spread (max - min; 0 where all are -inf, inf where they
-    disagree on -inf).  Returns (vals[4, B], spread[B])."""
+def reference_lnl(pta, X, exact="auto"):
+    """(enterprise-order lnL, near-exact lnL) of every row of X.  exact:
+    "dd" -- oracle/ddref.py (double-double, uncorrelated / CURN models),
+    "ext" -- the extended-precision restatement with an error-free Gram
+    (oracle/device_order_ref.py, np.longdouble), "auto" -- dd when the model
+    allows it and the pulsars are few."""
     from oracle.device_order_ref import DeviceOrderPTA
+    from oracle.ddref import DDReferencePTA
     from oracle.enterprise_ref import OraclePTA
     const = pta.constant_values()
     fixed = const if pta.white_fixed() else None
     psrs, terms = [c.psr for c in pta.signal_collections], pta.oracle_terms()
-    orcs = [OraclePTA(psrs, terms, fixed_params=fixed),
-            DeviceOrderPTA(psrs, terms, fixed, np.float64, gram_mode="blas"),
-            DeviceOrderPTA(psrs, terms, fixed, np.float64, gram_mode="reverse", factor="chol"),
-            DeviceOrderPTA(psrs, terms, fixed, np.longdouble)]
-    vals = np.empty((len(orcs), len(X)))
-    for i, o in enumerate(orcs):
-        for b, x in enumerate(X):
-            d = dict(const)
-            d.update(pta.map_params(x))
-            vals[i, b] = o.lnlikelihood(d)
-    fin = np.isfinite(vals)
-    spread = np.zeros(len(X))
-    allf = fin.all(axis=0)
-    spread[allf] = vals[:, allf].max(axis=0) - vals[:, allf].min(axis=0)
-    spread[~allf & fin.any(axis=0)] = np.inf
-    return vals, spread
+    ent = OraclePTA(psrs, terms, fixed_params=fixed)
+    if exact == "auto":
+        exact = "dd" if not ent.correlated() and len(psrs) <= 4 else "ext"
+    ref = DDReferencePTA(psrs, terms) if exact == "dd" else DeviceOrderPTA(psrs, terms, fixed, np.longdouble)
+    a, b = [], []
+    for x in X:
+        d = dict(const)
+        d.update(pta.map_params(x))
+        a.append(ent.lnlikelihood(d))
+        b.append(ref.lnlikelihood(d))
+    return np.array(a), np.array(b)
 
 
 def load_golden(name, full=False):
     """Rebuild (pta, theta, lnl, min_eig) from a committed fixture; full=True
-    returns (pta, z) with every stored array (lnl_dev, lnl_exact, spread, near)."""
+    returns (pta, z) with every stored array (lnl = enterprise order, lnl_dev
+    = the device's order in fp64, lnl_exact = near-exact, spread, near)."""
     from enterprise_warp_amd import synth
     from enterprise_warp_amd.pulsar import Pulsar
     z = np.load(os.path.join(GOLDEN, name + ".npz"), allow_pickle=False)

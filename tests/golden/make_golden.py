@@ -31,29 +31,37 @@ ORDERINGS = ("enterprise", "device", "device_blas", "reverse_chol", "extended")
 
 
 def oracle_lnl(pta, X):
-    """Per sample, the lnL of five correct orderings of the same likelihood:
+    """Per sample, the lnL of five orderings of the same likelihood:
       enterprise    oracle/enterprise_ref.py (the full Sigma by cho_factor)
-      device        the device's order (oracle/device_order_ref.py: the
-                    contraction kernels' FMA accumulation order for the Gram,
-                    schur_kernel's timing-model elimination, blocked LDL^T)
-      device_blas   the same with a BLAS Gram and a plain Schur step
-      reverse_chol  the Gram summed over the TOAs in reverse, unblocked Cholesky
-      extended      the device order in x87 extended precision (eps 1.1e-19):
-                    a near-exact value for the same fp64 inputs
-    and the measured spread = max - min of the five (0 where all are -inf; inf
-    where they disagree on -inf).  The GPU tests bound |gpu - ref| by
-    max(strict, 4 spread) (strict = 1e-6 + 1e-10 |lnL|, BASELINE.json) on
-    prior draws and by strict on near-truth draws.  Also returns the
+      device        the device's order (oracle/device_order_ref.py: projected
+                    basis, the contraction kernels' FMA accumulation order for
+                    a varying-white-noise Gram, double-double cache and
+                    timing-model elimination for fixed white noise, two-level
+                    blocked LDL^T)
+      device_blas   the same with a BLAS Gram
+      reverse_chol  original basis, the Gram summed over the TOAs in reverse,
+                    unblocked Cholesky
+      extended      near-exact: oracle/ddref.py (double-double) for
+                    uncorrelated / CURN models, the extended-precision
+                    restatement with an error-free Gram for correlated ones
+    and the spread = max - min of the five (informational; 0 where all are
+    -inf, inf where they disagree on -inf).  The GPU tests hold near-truth
+    draws to strict and prior draws to |gpu - extended| <= max(|enterprise -
+    extended|, strict) (tests/conftest.py check_accuracy).  Also returns the
     conditioning of what the device factors (informational)."""
+    from oracle.ddref import DDReferencePTA
     const = pta.constant_values()
     fixed = const if pta.white_fixed() else None
     psrs = [c.psr for c in pta.signal_collections]
     terms = pta.oracle_terms()
-    models = [OraclePTA(psrs, terms, fixed_params=fixed),
+    ent = OraclePTA(psrs, terms, fixed_params=fixed)
+    exact = (DeviceOrderPTA(psrs, terms, fixed, np.longdouble) if ent.correlated()
+             else DDReferencePTA(psrs, terms))
+    models = [ent,
               DeviceOrderPTA(psrs, terms, fixed, np.float64, gram_mode="device"),
               DeviceOrderPTA(psrs, terms, fixed, np.float64, gram_mode="blas"),
               DeviceOrderPTA(psrs, terms, fixed, np.float64, gram_mode="reverse", factor="chol"),
-              DeviceOrderPTA(psrs, terms, fixed, np.longdouble)]
+              exact]
     vals = np.zeros((len(models), len(X)))
     cond = []
     for j, x in enumerate(X):
@@ -61,7 +69,7 @@ def oracle_lnl(pta, X):
         d.update(pta.map_params(x))
         for i, mdl in enumerate(models):
             vals[i, j] = mdl.lnlikelihood(d)
-        cond.append(models[2].min_eig(d))
+        cond.append(models[3].min_eig(d))
     fin = np.isfinite(vals).all(axis=0)
     spread = np.zeros(len(X))
     spread[fin] = vals[:, fin].max(axis=0) - vals[:, fin].min(axis=0)

@@ -203,15 +203,18 @@ def test_device_order_matches_enterprise_order_near_truth(name):
 @pytest.mark.parametrize("name", GOLDEN_NAMES)
 def test_device_order_reproduces_golden(name):
     """DeviceOrderPTA (fp64, the device's accumulation order) regenerates the
-    stored lnl_dev bit for bit; the extended-precision form regenerates
+    stored lnl_dev bit for bit; the near-exact reference (double-double for
+    uncorrelated / CURN fixtures, extended precision otherwise) regenerates
     lnl_exact on two samples."""
+    from oracle.ddref import DDReferencePTA
     from oracle.device_order_ref import DeviceOrderPTA
     pta, z = load_golden(name, full=True)
     const_ = pta.constant_values()
     fixed = const_ if pta.white_fixed() else None
     psrs = [c.psr for c in pta.signal_collections]
     d64 = DeviceOrderPTA(psrs, pta.oracle_terms(), fixed, np.float64, gram_mode="device")
-    dld = DeviceOrderPTA(psrs, pta.oracle_terms(), fixed, np.longdouble)
+    exact = (DeviceOrderPTA(psrs, pta.oracle_terms(), fixed, np.longdouble) if d64.correlated()
+             else DDReferencePTA(psrs, pta.oracle_terms()))
     rows = range(len(z["theta"])) if fixed is not None else range(0, len(z["theta"]), 4)   # (varying WN: slow)
     for i in rows:
         x = z["theta"][i]
@@ -221,7 +224,44 @@ def test_device_order_reproduces_golden(name):
         want = z["lnl_dev"][i]
         assert got == want or (not np.isfinite(want) and got == want)
         if i in (0, 8):
-            assert dld.lnlikelihood(d) == z["lnl_exact"][i]
+            assert exact.lnlikelihood(d) == z["lnl_exact"][i]
+
+
+@pytest.mark.parametrize("name", ["c1_turnover", "c1_system"])
+def test_double_double_reference_agrees_with_extended(name):
+    """The two near-exact references -- double-double (oracle/ddref.py) and
+    the extended-precision restatement with an error-free Gram -- agree to
+    within 0.5 x strict on every golden sample, including the ill-conditioned
+    prior draws where enterprise's fp64 order is 1e1-1e3 x strict off."""
+    from conftest import strict_tolerance
+    from oracle.device_order_ref import DeviceOrderPTA
+    pta, z = load_golden(name, full=True)
+    const_ = pta.constant_values()
+    fixed = const_ if pta.white_fixed() else None
+    ld = DeviceOrderPTA([c.psr for c in pta.signal_collections], pta.oracle_terms(), fixed, np.longdouble)
+    for i, x in enumerate(z["theta"]):
+        d = dict(const_)
+        d.update(pta.map_params(x))
+        assert abs(ld.lnlikelihood(d) - z["lnl_exact"][i]) <= 0.5 * strict_tolerance(z["lnl_exact"][i])
+
+
+def test_exact_gram_and_two_prod():
+    """Error-free transformations of the references: TwoProduct is exact, and
+    the sliced (Ozaki) Gram matches an extended-precision product to ~1e-18
+    of sqrt(G_ii G_jj) on a column pair that cancels to 1e-9."""
+    from oracle.device_order_ref import exact_gram, two_prod
+    rng = np.random.default_rng(0)
+    a, b = rng.standard_normal(1000), rng.standard_normal(1000)
+    p, e = two_prod(a, b)
+    assert np.all(p.astype(np.longdouble) + e == a.astype(np.longdouble) * b)
+    X = rng.standard_normal((3000, 12)) * np.exp(rng.uniform(-20, 5, 12))[None, :]
+    X[:, 3] = X[:, 4] * (1 + 1e-9)
+    D = np.exp(rng.uniform(-30, -20, 3000)).astype(np.longdouble)
+    G1 = exact_gram(X, D)
+    Xl = X.astype(np.longdouble)
+    G2 = Xl.T @ (Xl / D[:, None])
+    rel = np.abs(G1 - G2) / np.sqrt(np.outer(np.diag(G2), np.diag(G2)))
+    assert float(rel.max()) < 1e-17
 
 
 def test_device_order_extended_precision_is_closer_on_ill_conditioned_draws():
