@@ -123,6 +123,83 @@ def cpu_baseline(seconds, procs=None):
                       f"= {sum(k for k, _ in res)} evaluations; value = the better mode"}
 
 
+def contraction_work(pta):
+    """SURVEY.md §8(d) per (pulsar, sample), varying white noise: algorithmic
+    flops of T^T N^-1 T, T^T N^-1 r, r^T N^-1 r, log|N| (+ ECORR terms) --
+    F = n m (m + 1) + 2 n m + 3 n + 2 n (m + 1) + E (m + 1)^2 -- and the bytes
+    the N-weighted basis read streams: B_bytes = 8 n m + 20 n (T, r, sigma,
+    backend and epoch indices once per sample; B_tile = 1).  Summed over
+    pulsars."""
+    flops = bytes_ = 0.0
+    for c in pta.signal_collections:
+        n, m = c.T.shape
+        E = len(c.ecorr_epochs())
+        flops += n * m * (m + 1) + 2 * n * m + 3 * n + (2 * n * (m + 1) + E * (m + 1) ** 2 if E else 0)
+        bytes_ += 8 * n * m + 20 * n
+    return flops, bytes_
+
+
+def secondary_configs(dev, steps=5):
+    """BASELINE configs 2 and 4 (white noise varying every call), measured in
+    this run on this GPU: lnL evals/s of the full batch (ewh_lnl_units_device,
+    HIP events around `steps` launches) and, for the contraction stage alone
+    (ewh_contract_device: N^-1, ECORR, the fp64 MFMA T^T N^-1 T), its
+    algorithmic fp64 rate against the MFMA peak and the N-weighted basis
+    stream in GB/s against HBM peak."""
+    import torch
+    from enterprise_warp_amd import synth
+    out = {}
+    for name, make in (("c2", synth.config_c2), ("c4", synth.config_c4)):
+        cfg = make()
+        pta, B = cfg.pta, cfg.B
+        X = synth.prior_draws(pta, B, cfg.theta_seed)
+        th = torch.from_numpy(X).to(dev)
+        eng = pta.engine(device=dev.index)
+        U = len(pta.signal_collections) * B
+        res = torch.zeros(B, dtype=torch.float64, device=dev)
+        st = torch.cuda.current_stream(dev)
+
+        def timed(fn):
+            fn()
+            torch.cuda.synchronize(dev)
+            a, b = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+            a.record(st)
+            for _ in range(steps):
+                fn()
+            b.record(st)
+            torch.cuda.synchronize(dev)
+            return a.elapsed_time(b) / steps
+
+        ms = timed(lambda: eng.lnl_units_device(th.data_ptr(), B, 0, U, res.data_ptr(), st.cuda_stream))
+        cms = timed(lambda: eng.contract_device(th.data_ptr(), B, st.cuda_stream))
+        f, by = contraction_work(pta)
+        tf = f * B / (cms * 1e-3) / 1e12
+        gbs = by * B / (cms * 1e-3) / 1e9
+        out[name] = {"evals_per_s": B / (ms * 1e-3), "ms_per_batch": ms, "batch": B,
+                     "finite_fraction": float(np.mean(np.isfinite(res.cpu().numpy()))),
+                     "contraction": {"ms": cms, "share_of_batch": cms / ms,
+                                     "algorithmic_tflops": tf, "fp64_mfma_frac": tf / FP64_MFMA_PEAK_TFLOPS,
+                                     "basis_stream_GBs": gbs, "hbm_frac": gbs / HBM_PEAK_GBS,
+                                     "flops_per_sample": f, "bytes_per_sample": by}}
+        pta._drop_engine()
+        del th, res
+    out["note"] = ("configs 2 and 4 at their stated sizes, prior draws, white noise varying every call; "
+                   "contraction = ewh_contract_device alone (wn_weights + contract2_kernel); the basis stream "
+                   "is the algorithmic bytes each sample's workgroup reads (T is L2/MALL resident across samples)")
+    return out
+
+
+def kernel_sources_sha():
+    """sha256 of the sources of the factorisation kernel (ewarp_dev.h and its
+    instantiating translation unit): ties a committed PMC profile to this tree."""
+    import hashlib
+    hsh = hashlib.sha256()
+    for f in ("ewarp_dev.h", "chol_small.hip"):
+        with open(os.path.join(ROOT, "enterprise_warp_amd", "csrc", f), "rb") as fh:
+            hsh.update(fh.read())
+    return hsh.hexdigest()[:16]
+
+
 def sampler_latency(pta, cfg, batches=(1, 16, 256), reps=50):
     """The drop-in as samplers call it: host theta in, host lnL out through
     ewh_lnl_batch (pinned staging, H2D, launches, D2H, stream sync), one
@@ -161,6 +238,7 @@ def main():
     ap.add_argument("--cpu-procs", type=int, default=None, help="default: every usable core (affinity / cgroup quota)")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-latency", action="store_true")
+    ap.add_argument("--no-secondary", action="store_true", help="skip the C2 / C4 secondary measurements")
     ap.add_argument("--kernel-mode", type=int, default=0, help="0 auto (MFMA), 1 LDS fallback")
     ap.add_argument("--config", default="c3", choices=["c3", "c5"],
                     help="c3: the headline 45-pulsar CURN batch (default); c5: 100-pulsar HD-correlated PTA")
@@ -285,15 +363,25 @@ def main():
         lo, hi = max(u0, p * B), min(u1, (p + 1) * B)
         flops += max(0, hi - lo) * f_unit[p]
     achieved = flops / (launch_ms * 1e-3) / 1e12
-    traffic = None
+    # HBM bytes per launch of this kernel from the committed PMC pass, used
+    # only when that pass profiled these very kernel sources (sha match)
+    traffic, traffic_src = None, None
     pmc = os.path.join(ROOT, "profiles", "pmc_chol.json")
     if os.path.exists(pmc):
         with open(pmc) as fh:
-            traffic = json.load(fh).get("hbm_bytes_per_launch")
+            rec_pmc = json.load(fh)
+        if rec_pmc.get("kernel_sources_sha") == kernel_sources_sha():
+            traffic = rec_pmc.get("hbm_bytes_per_launch")
+            traffic_src = f"profiles/{rec_pmc.get('tag')}/pmc_summary.json (kernel sources sha " \
+                          f"{rec_pmc['kernel_sources_sha']})"
 
     latency = None
     if rank == 0 and not args.no_latency:
         latency = sampler_latency(pta, cfg)
+    secondary = None
+    if rank == 0 and world == 1 and not args.no_secondary:
+        pta._drop_engine()
+        secondary = secondary_configs(dev)
     if rank == 0:
         value = B * args.steps / elapsed
         rec = {
@@ -306,10 +394,15 @@ def main():
                        "global_batch": B, "batch_per_gpu": args.batch_per_gpu, "n_pulsars": len(m_psr),
                        "parallelism": f"units{world}", "finite_fraction": float(np.mean(np.isfinite(lnl)))},
             "roofline": {"bound": "mfma", "achieved": achieved, "peak": FP64_MFMA_PEAK_TFLOPS, "unit": "TFLOP/s",
-                         "frac": achieved / FP64_MFMA_PEAK_TFLOPS, "traffic": traffic,
-                         "kernel": "chol_mfma_kernel<8,1,2,23> (blocked LDL^T panel: diagonal block by fused DPP multiply-adds, row by MFMA with L^-1)", "launch_ms": launch_ms,
+                         "frac": achieved / FP64_MFMA_PEAK_TFLOPS, "traffic": traffic, "traffic_source": traffic_src,
+                         "kernel": "chol_mfma_kernel<8,2,25> (two-level blocked LDL^T panel: 4-row sub-panels by "
+                                   "fused DPP multiply-adds, each closed by one MFMA rank-4 update; rest of the "
+                                   "block row by MFMA with L^-1)",
+                         "kernel_sources_sha": kernel_sources_sha(), "launch_ms": launch_ms,
                          "flops_per_launch": flops},
         }
+        if secondary is not None:
+            rec["secondary"] = secondary
         if cpu is not None:
             rec["cpu_baseline"] = cpu
             rec["gpu_over_cpu"] = {"per_gpu": value / world / cpu["value"],

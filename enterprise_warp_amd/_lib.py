@@ -53,8 +53,8 @@ class PtaDesc(C.Structure):
 
 EXPORTS = ["ewh_create", "ewh_num_devices", "ewh_set_fixed_white", "ewh_lnl_batch", "ewh_lnl_units_device",
            "ewh_keep_dim", "ewh_corr_partial_device", "ewh_corr_finish_device",
-           "ewh_last_unit_terms", "ewh_unit_cost", "ewh_set_kernel_mode", "ewh_optstat", "ewh_destroy",
-           "ewh_last_error", "ewh_version"]
+           "ewh_last_unit_terms", "ewh_unit_cost", "ewh_set_kernel_mode", "ewh_optstat", "ewh_contract_device",
+           "ewh_destroy", "ewh_last_error", "ewh_version"]
 DEV_EXPORTS = ["ewh_dev_gram", "ewh_dev_reduced"]
 
 _lib = None
@@ -108,6 +108,8 @@ def load():
     lib.ewh_set_kernel_mode.restype = C.c_int
     lib.ewh_optstat.argtypes = [C.c_void_p, _dp, C.c_int32, _dp, _dp, _dp, _dp, _dp]
     lib.ewh_optstat.restype = C.c_int
+    lib.ewh_contract_device.argtypes = [C.c_void_p, C.c_void_p, C.c_int32, C.c_void_p]
+    lib.ewh_contract_device.restype = C.c_int
     lib.ewh_destroy.argtypes = [C.c_void_p]
     lib.ewh_destroy.restype = None
     lib.ewh_last_error.argtypes = []

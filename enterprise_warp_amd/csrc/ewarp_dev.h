@@ -230,7 +230,22 @@ struct CholJob {
   const int* rep = nullptr;
   const int* ulist = nullptr;
   int nu = 0;
+  // the same, staged for the register kernels' prologue: one record per
+  // distinct spectrum with its entries inline (URec), and per column the
+  // record it takes (urep, -1 = no entry); theta is read from LDS.  One
+  // global-load level instead of four (ulist -> col_ptr -> spec -> theta).
+  // NULL: the CSR path (a spectrum with more than URec::NE entries)
+  const struct URec* urec = nullptr;
+  const int* urep = nullptr;
 };
+
+// one distinct spectrum of a fixed-WN job: phi = sum of its ne entries
+struct URec {
+  static constexpr int NE = 3;
+  DSpec e[NE];
+  int ne, pad_[3];
+};
+constexpr int STAGE_THETA_MAX = 512;   // theta row staged in LDS up to this many parameters
 
 // ----------------------------------------------------------------------------
 // fp64 MFMA contraction G = T_aug^T W T_aug - sum_e beta_e s_e s_e^T
@@ -711,14 +726,18 @@ __device__ __forceinline__ void panel_ldl_row(BBt BBc, Blk&& blk, int q, int c, 
                                               const Hook& hook = Hook{}, int klim = 16) {
   constexpr int bb = decltype(BBc)::value;
   constexpr bool TWO = ALG == PANEL_2L;
-  static_assert(ALG == PANEL_1L || ALG == PANEL_2L, "unknown panel form");
+  static_assert(ALG == PANEL_1L || TWO, "unknown panel form");
   constexpr bool LASTR = RL && bb == NB - 1;          // block row holding the residual
   v4d E;
   static_for<0, 4>([&](auto R) {
     constexpr int r = decltype(R)::value;
     E[r] = (q + 4 * r == c) ? 1.0 : 0.0;
   });
-  // two-level: the row scales D^-1/2 of sub-panel s, formed when it closes
+  // two-level: the row scales D^-1/2 of sub-panel s, formed when it closes.
+  // (Folding them into E's columns instead -- E D^-1/2, one gather, four
+  // multiplies -- was tried in round 3: the wide chol_big_kernel and the
+  // one-wave NB = 9 kernel then faulted with an illegal address on the GPU;
+  // not kept.)
   double rsr[4] = {1.0, 1.0, 1.0, 1.0};
   static_for<0, 4>([&](auto KR) {
     constexpr int kr = decltype(KR)::value;
@@ -879,32 +898,65 @@ void chol_mfma_kernel(const CholJob* __restrict__ jobs, int B, long long u0, int
       pre[decltype(BJ)::value][r] = A[(long long)(q + 4 * r) * LD + 16 * decltype(BJ)::value + c];
     });
   });
-  const bool dedup = J.rep != nullptr;
-  if (dedup) {
-    for (int i = lane; i < J.nu; i += 64) {
-      const int a = J.ulist[i];
-      double ph = 0.0;
-      for (int e = J.col_ptr[a]; e < J.col_ptr[a + 1]; ++e) ph += spec_phi_body(J.spec[e], th);
-      phs[a] = ph;
-    }
-    __syncthreads();
-  }
   // log|phi| is summed into the per-lane log-det accumulator (one log() at
   // the end of the kernel)
   LogAcc ldet;
-  for (int a = lane; a < LD; a += 64) {
-    double pi = 0.0;
-    if (a < J.mreal && J.col_ptr[a] < J.col_ptr[a + 1]) {   // (pads carry no entry)
+  if (J.urec != nullptr && ldth <= STAGE_THETA_MAX) {
+    // staged: theta row -> LDS, each distinct spectrum's record by its lane,
+    // every column's record index -- all loads issued together
+    __shared__ double ths[STAGE_THETA_MAX];
+    int ur[(LD + 63) / 64];
+    static_for<0, (LD + 63) / 64>([&](auto I) {
+      constexpr int i = decltype(I)::value;
+      ur[i] = 64 * i + lane < J.mreal ? J.urep[64 * i + lane] : -1;
+    });
+    for (int i = lane; i < ldth; i += 64) ths[i] = th[i];
+    __syncthreads();
+    for (int u = lane; u < J.nu; u += 64) {
+      const URec& R = J.urec[u];
       double ph = 0.0;
-      if (dedup) {
-        ph = phs[J.rep[a]];
-      } else {
-        for (int e = J.col_ptr[a]; e < J.col_ptr[a + 1]; ++e) ph += spec_phi_body(J.spec[e], th);
-      }
-      pi = 1.0 / ph;
-      ldet.add(ph);
+      for (int e = 0; e < R.ne; ++e) ph += spec_phi_body(R.e[e], ths);
+      phs[u] = ph;
     }
-    phinv[a] = pi;
+    __syncthreads();
+    static_for<0, (LD + 63) / 64>([&](auto I) {
+      constexpr int i = decltype(I)::value;
+      const int a = 64 * i + lane;
+      if (a < LD) {
+        double pi = 0.0;
+        if (ur[i] >= 0) {
+          const double ph = phs[ur[i]];
+          pi = 1.0 / ph;
+          ldet.add(ph);
+        }
+        phinv[a] = pi;
+      }
+    });
+  } else {
+    const bool dedup = J.rep != nullptr;
+    if (dedup) {
+      for (int i = lane; i < J.nu; i += 64) {
+        const int a = J.ulist[i];
+        double ph = 0.0;
+        for (int e = J.col_ptr[a]; e < J.col_ptr[a + 1]; ++e) ph += spec_phi_body(J.spec[e], th);
+        phs[a] = ph;
+      }
+      __syncthreads();
+    }
+    for (int a = lane; a < LD; a += 64) {
+      double pi = 0.0;
+      if (a < J.mreal && J.col_ptr[a] < J.col_ptr[a + 1]) {   // (pads carry no entry)
+        double ph = 0.0;
+        if (dedup) {
+          ph = phs[J.rep[a]];
+        } else {
+          for (int e = J.col_ptr[a]; e < J.col_ptr[a + 1]; ++e) ph += spec_phi_body(J.spec[e], th);
+        }
+        pi = 1.0 / ph;
+        ldet.add(ph);
+      }
+      phinv[a] = pi;
+    }
   }
   __syncthreads();
   EWH_STAMP(1)

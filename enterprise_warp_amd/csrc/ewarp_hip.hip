@@ -1096,6 +1096,16 @@ __global__ void reduce_units_kernel(const double* __restrict__ units, int P, int
   out[b] = s;
 }
 
+// Multi-context handle: out[b] = sum_i part[i * B + b], the contexts' partial
+// sums (each over its unit range, pulsars in order) in context order.
+__global__ void fold_partials_kernel(const double* __restrict__ part, int nd, int B, double* __restrict__ out) {
+  const int b = blockIdx.x * blockDim.x + threadIdx.x;
+  if (b >= B) return;
+  double s = 0.0;
+  for (int i = 0; i < nd; ++i) s += part[(long long)i * B + b];
+  out[b] = s;
+}
+
 }  // namespace ewh_dev
 
 using namespace ewh_dev;
@@ -1119,6 +1129,8 @@ struct PsrHost {
   int* d_fx_rep = nullptr;        // fixed columns -> first column with the same spectrum
   int* d_fx_ulist = nullptr;      // the distinct-spectrum columns
   int fx_nu = 0;
+  URec* d_fx_urec = nullptr;      // the distinct spectra with their entries inline (NULL: > URec::NE entries)
+  int* d_fx_urep = nullptr;       // fixed columns -> distinct-spectrum record (-1: no entry)
   double* d_S = nullptr;          // fx_ld^2
   bool has_theta_white = false;
   int n_slot = 0;
@@ -1133,6 +1145,7 @@ struct DevCtx {
   int P = 0, n_param = 0;
   bool white_fixed = false;
   int kernel_mode = 0;
+  bool stage_spectra = true;   // register kernels read the staged spectrum records (dev mode 19: the CSR path)
   hipStream_t stream = nullptr;
   std::vector<PsrHost> psr;
   std::vector<void*> allocs;
@@ -1545,7 +1558,7 @@ int setup_fixed(DevCtx* h) {
     // with entries (optimal statistic: the CURN Sigma of each pulsar)
     const int mreal = h->osmode ? ps.fx_ld - 1 : ps.nloc;
     jobs[p] = CholJob{ps.d_S, 0, ps.fx_ld, mreal, ps.d_fx_colptr, ps.d_fx_spec, h->d_fxK + p, 0, 0,
-                      ps.d_fx_rep, ps.d_fx_ulist, ps.fx_nu};
+                      ps.d_fx_rep, ps.d_fx_ulist, ps.fx_nu, h->stage_spectra ? ps.d_fx_urec : nullptr, ps.d_fx_urep};
   }
   EWH_HIP(hipMemcpyAsync(fails.data(), h->d_fxfail, sizeof(int) * h->P, hipMemcpyDeviceToHost, h->stream));
   EWH_HIP(hipStreamSynchronize(h->stream));
@@ -1965,6 +1978,25 @@ int create_ctx(const ewh_pta_desc* d, const std::vector<ProjCoef>& proj, int dev
       std::vector<int> rep, ulist;
       build_spec_rep(ptr, ent, rep, ulist);
       ps.fx_nu = (int)ulist.size();
+      // staged records: ulist order; urep[a] = record of column a's spectrum
+      std::vector<int> urep(rep.size(), -1), uidx(rep.size(), -1);
+      for (size_t u = 0; u < ulist.size(); ++u) uidx[ulist[u]] = (int)u;
+      bool fits = true;
+      std::vector<URec> urec(std::max<size_t>(1, ulist.size()));
+      for (size_t u = 0; u < ulist.size(); ++u) {
+        const int a = ulist[u];
+        const int ne = ptr[a + 1] - ptr[a];
+        if (ne > URec::NE) fits = false;
+        urec[u] = URec{};
+        urec[u].ne = std::min(ne, URec::NE);
+        for (int e = 0; e < urec[u].ne; ++e) urec[u].e[e] = ent[ptr[a] + e];
+      }
+      for (size_t a = 0; a < rep.size(); ++a)
+        if (ptr[a] < ptr[a + 1]) urep[a] = uidx[rep[a]];
+      if (fits) {
+        if ((rc = dupload(h, &ps.d_fx_urec, urec.data(), urec.size()))) return bail(rc);
+        if ((rc = dupload(h, &ps.d_fx_urep, urep.data(), urep.size()))) return bail(rc);
+      }
       if (ulist.empty()) ulist.push_back(0);
       if ((rc = dupload(h, &ps.d_fx_rep, rep.data(), rep.size()))) return bail(rc);
       if ((rc = dupload(h, &ps.d_fx_ulist, ulist.data(), ulist.size()))) return bail(rc);
@@ -2197,6 +2229,11 @@ struct ewh_handle {
   // sample range (correlated)
   std::vector<std::pair<long long, long long>> last_split;
   int last_B = 0;
+  // multi-context fold on the first context's device: per-context partial
+  // B-vectors (peer-copied in), and one event per context
+  double* d_part = nullptr;
+  size_t part_cap = 0;
+  std::vector<hipEvent_t> ev;
 };
 
 namespace {
@@ -2251,13 +2288,18 @@ int lnl_batch_corr_pulsars(ewh_handle* H, int B, double* out_host) {
   }
   EWH_HIP(hipSetDevice(h0->device));
   EWH_HIP(hipMemsetAsync(h0->d_units, 0, sizeof(double) * (size_t)(P + 1) * B, h0->stream));
+  // theta on the first device always: corr_finish reads it there even when
+  // the first context gets no pulsars (P < number of contexts)
+  if (np > 0)
+    EWH_HIP(hipMemcpyAsync(h0->d_theta, H->h_theta, sizeof(double) * (size_t)B * np, hipMemcpyHostToDevice,
+                           h0->stream));
   EWH_HIP(hipStreamSynchronize(h0->stream));
   for (int i = 0; i < nd; ++i) {
     DevCtx* h = H->ctx[i];
     const int p0 = (int)((long long)P * i / nd), p1 = (int)((long long)P * (i + 1) / nd);
     if (p1 <= p0) continue;
     EWH_HIP(hipSetDevice(h->device));
-    if (np > 0)
+    if (np > 0 && i > 0)
       EWH_HIP(hipMemcpyAsync(h->d_theta, H->h_theta, sizeof(double) * (size_t)B * np, hipMemcpyHostToDevice,
                              h->stream));
     if ((rc = corr_partial(h, h->d_theta, B, p0, p1, h->d_units, h->d_keep, h->stream))) return rc;
@@ -2407,6 +2449,14 @@ int ewh_set_kernel_mode(ewh_handle* H, int32_t mode) {
     h->kernel_mode = mode;
     (void)hipSetDevice(h->device);
     drop_graphs(h);
+    const bool stage = mode != 19;   // dev mode 19: the register kernels' CSR spectrum prologue
+    if (stage != h->stage_spectra) {
+      h->stage_spectra = stage;
+      if (h->white_fixed) {
+        const int rc = setup_fixed(h);
+        if (rc) return rc;
+      }
+    }
   }
   return 0;
 }
@@ -2432,39 +2482,50 @@ int ewh_lnl_batch(ewh_handle* H, const double* theta_host, int32_t B, double* ou
   if (!H || !theta_host || !out_host || B <= 0) return set_err(EWH_E_INVALID, "bad arguments");
   if (H->ctx[0]->osmode) return set_err(EWH_E_UNSUPPORTED, "an optimal-statistic handle evaluates ewh_optstat only");
   const int nd = (int)H->ctx.size(), np = H->n_param;
-  const long long U = (long long)H->P * B;
   int rc;
   if ((rc = ensure_pinned(&H->h_theta, &H->h_theta_cap, (size_t)B * std::max(1, np)))) return rc;
   if (np > 0) std::memcpy(H->h_theta, theta_host, sizeof(double) * (size_t)B * np);
   if (nd == 1) return lnl_batch_single(H, H->ctx[0], B, out_host);
   if (H->corr && B < nd) return lnl_batch_corr_pulsars(H, B, out_host);
   std::vector<std::pair<long long, long long>> split;
-  if (nd == 1 || H->corr) {
-    // samples: contiguous slices (correlated: the cross-pulsar factorisation
-    // needs every pulsar of a sample on one device)
+  if (H->corr) {
+    // samples: contiguous slices (the cross-pulsar factorisation needs every
+    // pulsar of a sample on one device)
     for (int i = 0; i < nd; ++i) split.push_back({(long long)B * i / nd, (long long)B * (i + 1) / nd});
-    if ((rc = ensure_pinned(&H->h_out, &H->h_out_cap, (size_t)B))) return rc;
   } else {
     std::vector<double> cost(H->P);
     for (int p = 0; p < H->P; ++p) cost[p] = ctx_unit_cost(H->ctx[0], p);
     split = unit_ranges(cost, B, nd);
-    if ((rc = ensure_pinned(&H->h_out, &H->h_out_cap, (size_t)U))) return rc;
   }
-  const bool by_units = !(nd == 1 || H->corr);
+  if ((rc = ensure_pinned(&H->h_out, &H->h_out_cap, (size_t)B))) return rc;
+  DevCtx* h0 = H->ctx[0];
+  if (!H->corr) {
+    // per-context partial sums are folded on the first device: a partial
+    // B-vector per context there, one event per context
+    EWH_HIP(hipSetDevice(h0->device));
+    const size_t need = (size_t)nd * B;
+    if (need > H->part_cap) {
+      if (H->d_part) (void)hipFree(H->d_part);
+      H->d_part = nullptr;
+      H->part_cap = 0;
+      hipError_t e = hipMalloc((void**)&H->d_part, need * sizeof(double));
+      if (e != hipSuccess) return set_err(EWH_E_NOMEM, std::string("hipMalloc: ") + hipGetErrorString(e));
+      H->part_cap = need;
+    }
+    while ((int)H->ev.size() < nd) {
+      const int i = (int)H->ev.size();
+      EWH_HIP(hipSetDevice(H->ctx[i]->device));
+      hipEvent_t e;
+      EWH_HIP(hipEventCreateWithFlags(&e, hipEventDisableTiming));
+      H->ev.push_back(e);
+    }
+  }
   for (int i = 0; i < nd; ++i) {
     DevCtx* h = H->ctx[i];
     const long long a = split[i].first, b = split[i].second;
-    if (b <= a) continue;
     EWH_HIP(hipSetDevice(h->device));
-    if (by_units) {
-      if ((rc = ensure_io(h, B))) return rc;
-      if (np > 0)
-        EWH_HIP(hipMemcpyAsync(h->d_theta, H->h_theta, sizeof(double) * (size_t)B * np, hipMemcpyHostToDevice,
-                               h->stream));
-      if ((rc = ctx_units(h, h->d_theta, B, a, b, h->d_out, h->stream, false))) return rc;
-      EWH_HIP(hipMemcpyAsync(H->h_out + a, h->d_units + a, sizeof(double) * (size_t)(b - a), hipMemcpyDeviceToHost,
-                             h->stream));
-    } else {
+    if (H->corr) {
+      if (b <= a) continue;
       const int Bd = (int)(b - a);
       if ((rc = ensure_io(h, Bd))) return rc;
       if (np > 0)
@@ -2472,27 +2533,55 @@ int ewh_lnl_batch(ewh_handle* H, const double* theta_host, int32_t B, double* ou
                                hipMemcpyHostToDevice, h->stream));
       if ((rc = ctx_units(h, h->d_theta, Bd, 0, (long long)H->P * Bd, h->d_out, h->stream, true))) return rc;
       EWH_HIP(hipMemcpyAsync(H->h_out + a, h->d_out, sizeof(double) * Bd, hipMemcpyDeviceToHost, h->stream));
+    } else {
+      // every context evaluates its unit range and sums it over its pulsars
+      // (rows outside the range are zero) into a B-vector, which goes to the
+      // first device; only B doubles ever come back to the host
+      if ((rc = ensure_io(h, B))) return rc;
+      if (b > a && np > 0)
+        EWH_HIP(hipMemcpyAsync(h->d_theta, H->h_theta, sizeof(double) * (size_t)B * np, hipMemcpyHostToDevice,
+                               h->stream));
+      if ((rc = ctx_units(h, h->d_theta, B, a, b, h->d_out, h->stream, true))) return rc;
+      EWH_HIP(hipMemcpyPeerAsync(H->d_part + (size_t)i * B, h0->device, h->d_out, h->device, sizeof(double) * B,
+                                 h->stream));
+      EWH_HIP(hipEventRecord(H->ev[i], h->stream));
     }
   }
-  for (int i = 0; i < nd; ++i) {
-    if (split[i].second <= split[i].first) continue;
-    EWH_HIP(hipSetDevice(H->ctx[i]->device));
-    EWH_HIP(hipStreamSynchronize(H->ctx[i]->stream));
-  }
-  if (by_units) {
-    // sum over pulsars in pulsar order: the same left fold as reduce_units_kernel,
-    // so any split gives the single-device result bit for bit
-    for (int b = 0; b < B; ++b) {
-      double s = 0.0;
-      for (int p = 0; p < H->P; ++p) s += H->h_out[(size_t)p * B + b];
-      out_host[b] = s;
-    }
+  if (!H->corr) {
+    EWH_HIP(hipSetDevice(h0->device));
+    for (int i = 1; i < nd; ++i) EWH_HIP(hipStreamWaitEvent(h0->stream, H->ev[i], 0));
+    hipLaunchKernelGGL(fold_partials_kernel, dim3((B + 255) / 256), dim3(256), 0, h0->stream, H->d_part, nd, B,
+                       h0->d_out);
+    EWH_HIP(hipGetLastError());
+    EWH_HIP(hipMemcpyAsync(H->h_out, h0->d_out, sizeof(double) * B, hipMemcpyDeviceToHost, h0->stream));
+    EWH_HIP(hipStreamSynchronize(h0->stream));
   } else {
-    std::memcpy(out_host, H->h_out, sizeof(double) * B);
+    for (int i = 0; i < nd; ++i) {
+      if (split[i].second <= split[i].first) continue;
+      EWH_HIP(hipSetDevice(H->ctx[i]->device));
+      EWH_HIP(hipStreamSynchronize(H->ctx[i]->stream));
+    }
   }
+  std::memcpy(out_host, H->h_out, sizeof(double) * B);
   H->last_split = split;
   H->last_B = B;
   return 0;
+}
+
+int ewh_contract_device(ewh_handle* H, const double* theta_dev, int32_t B, void* stream) {
+  if (!H || !theta_dev || B <= 0) return set_err(EWH_E_INVALID, "bad arguments");
+  DevCtx* h = H->ctx[0];
+  if (h->white_fixed || h->corr || h->osmode)
+    return set_err(EWH_E_UNSUPPORTED, "ewh_contract_device: white noise must vary (uncorrelated / CURN handle)");
+  EWH_HIP(hipSetDevice(h->device));
+  int rc;
+  if ((rc = ensure_var_scratch(h, B))) return rc;
+  hipStream_t saved = h->stream;
+  h->stream = (hipStream_t)stream;
+  for (int p = 0; p < h->P && !rc; ++p)
+    for (int c0 = 0; c0 < B && !rc; c0 += h->chunk) rc = run_white(h, p, theta_dev, h->n_param, c0, std::min(h->chunk, B - c0));
+  h->stream = saved;
+  return rc;
 }
 
 int ewh_keep_dim(const ewh_handle* H) {
@@ -2569,6 +2658,14 @@ int ewh_last_unit_terms(ewh_handle* H, double* out_host, int32_t B) {
 
 void ewh_destroy(ewh_handle* H) {
   if (!H) return;
+  for (size_t i = 0; i < H->ev.size(); ++i) {
+    (void)hipSetDevice(H->ctx[i]->device);
+    (void)hipEventDestroy(H->ev[i]);
+  }
+  if (H->d_part) {
+    (void)hipSetDevice(H->ctx[0]->device);
+    (void)hipFree(H->d_part);
+  }
   for (DevCtx* c : H->ctx) destroy_ctx(c);
   if (H->h_theta) (void)hipHostFree(H->h_theta);
   if (H->h_out) (void)hipHostFree(H->h_out);

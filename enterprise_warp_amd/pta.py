@@ -439,6 +439,12 @@ class Engine:
         _lib.check(self.lib.ewh_lnl_units_device(self.h, C.c_void_p(theta_ptr), int(B), int(u0), int(u1),
                                                  C.c_void_p(out_ptr), C.c_void_p(stream or 0)))
 
+    def contract_device(self, theta_ptr, B, stream=None):
+        """Measurement entry (ewh_contract_device): the white-noise stage of a
+        varying-white-noise batch alone (N^-1, ECORR, the fp64 MFMA
+        contraction), no factorisation."""
+        _lib.check(self.lib.ewh_contract_device(self.h, C.c_void_p(theta_ptr), int(B), C.c_void_p(stream or 0)))
+
     def keep_dim(self):
         """Side of the kept common block of one (pulsar, sample) (0 when the
         model has no correlated common process)."""

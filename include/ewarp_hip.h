@@ -181,10 +181,13 @@ int ewh_set_fixed_white(ewh_handle* h, const double* values);
 
 /* lnL for B samples: theta_host [B x n_param], out_host [B]. Synchronous.
  * Several devices: uncorrelated / CURN models split the (pulsar, sample)
- * units into cost-balanced contiguous ranges (one per device) and sum the
- * per-pulsar terms on the host in pulsar order (bit-identical to one
- * device); a correlated common process splits the samples.  theta is staged
- * through pinned host memory owned by the handle. */
+ * units into cost-balanced contiguous ranges (one per device); each device
+ * sums its range over its pulsars (pulsar order) into a B-vector, the
+ * B-vectors are peer-copied to the first device and added there in device
+ * order, and only B doubles return to the host (equal to one device at the
+ * strict bound, not bit for bit: the fold is re-associated).  A correlated
+ * common process splits the samples.  theta is staged through pinned host
+ * memory owned by the handle. */
 int ewh_lnl_batch(ewh_handle* h, const double* theta_host, int32_t B, double* out_host);
 
 /* Device variant (the handle's first device) on a contiguous range [unit_begin, unit_end) of units
@@ -197,6 +200,14 @@ int ewh_lnl_batch(ewh_handle* h, const double* theta_host, int32_t B, double* ou
 int ewh_lnl_units_device(ewh_handle* h, const double* theta_dev, int32_t B,
                          int64_t unit_begin, int64_t unit_end, double* out_dev,
                          void* stream);
+
+/* Measurement entry (bench.py): the white-noise stage of a varying-white-
+ * noise batch alone -- per pulsar and sample N^-1, the ECORR terms and the
+ * fp64 MFMA contraction G = T^T N^-1 T (with d, r^T N^-1 r) into the
+ * handle's scratch, no factorisation -- for B samples on the handle's first
+ * device, asynchronous on `stream`.  EWH_E_UNSUPPORTED for fixed white noise
+ * or a correlated process. */
+int ewh_contract_device(ewh_handle* h, const double* theta_dev, int32_t B, void* stream);
 
 /* Correlated common process, pulsar-partitioned (the exchange step of
  * one proposal spread over several GPUs, one process per
@@ -240,27 +251,22 @@ int ewh_last_unit_terms(ewh_handle* h, double* out_host, int32_t B);
 double ewh_unit_cost(const ewh_handle* h, int32_t pulsar);
 
 /* Kernel selection: 0 = auto (register-blocked MFMA factorisation with the
- * LDL^T panel when the reduced matrix fits -- up to NB = 8 the blocked panel:
- * diagonal block by VALU, the rest of the block row by MFMA with L^-1 --, LDS
- * kernel otherwise), 1 = force the LDS kernel, 2 = the round-1 MFMA kernel
- * (Cholesky panel, looped steps).  A/B variants for NB = 8 only (else as 0):
- * 3 = unblocked DPP panel at one wave per SIMD, 4 = LDL^T with looped steps,
- * 5 = LDL^T with u_i by ds_bpermute (unrolled), 6 = LDL^T with the row
- * broadcast through LDS, 8 = unblocked DPP panel with the pivot row's own
- * update exec-masked, 9 = unblocked DPP panel (every block of the row by
- * VALU), 10 = blocked panel with the quotients by two Newton steps on the
- * hardware rcp estimate (the default uses one cubic correction), 11 = the
- * default plus row scales by one cubic rsq correction, 12 = the default
- * without the packed phase-3 row scales (four gathers + rsqrts per block row
- * instead of one), 13 = phase split H = 3 with every row scale packed,
- * 14 = ALG 8 + lookahead; 15 / 16 = the pipelined contraction with 4 / 8
- * waves per sample (default: 8 for 144+ columns, else 4).
- * 7 = default Cholesky with the round-1 kernels elsewhere: the
- * contraction (varying white noise: separate epoch-sum kernel, unpipelined
- * tiles) instead of the pipelined one and, for a correlated common process,
- * the right-looking dense update and the LDS Gauss-Jordan M_g inverse.
- * Modes 3-6 and 8-29 exist only in the dev library (`make dev`:
- * libewarp_hip_dev.so); the product library returns EWH_E_UNSUPPORTED. */
+ * two-level LDL^T panel -- the 16x16 diagonal block in 4-row sub-panels by
+ * VALU, each closed by one symmetric MFMA rank-4 update, the rest of the
+ * block row by MFMA with L^-1 -- when the matrix fits registers; the LDS
+ * kernel otherwise), 1 = force the LDS kernel (unblocked Cholesky; for a
+ * correlated common process also the round-1 dense LDS diagonal-block and
+ * panel kernels), 7 = default factorisation with the round-1 kernels
+ * elsewhere: the contraction (varying white noise: separate epoch-sum
+ * kernel, unpipelined tiles) instead of the pipelined one and, for a
+ * correlated common process, the right-looking dense update and the LDS
+ * Gauss-Jordan M_g inverse.
+ * Dev library only (`make dev`: libewarp_hip_dev.so): 15 / 16 = the
+ * pipelined contraction with 4 / 8 waves per sample (default: 8 for 144+
+ * columns, else 4), 17 = the round-2 one-level panel (NB = 8), 19 = the default with the spectra read through the CSR tables
+ * instead of the staged records, 21 = the default with in-kernel phase
+ * stamps (NB = 8, ewh_dev_stamps).  Other modes
+ * return EWH_E_UNSUPPORTED. */
 int ewh_set_kernel_mode(ewh_handle* h, int32_t mode);
 
 void ewh_destroy(ewh_handle* h);

@@ -1,0 +1,7 @@
+set -u
+cd "${GRAFT_REPO_ROOT:-/root/repo}"; mkdir -p gpurun_out; export TMPDIR=/tmp
+timeout -k 10 400 python scripts/chol_ab.py --rounds 7 --modes 0,18,19,17 > gpurun_out/chol_ab.log 2>&1; rc=$?; echo ab rc=$rc; grep -E '"(prior|near)/mode|median_ms|max_err' gpurun_out/chol_ab.log | paste - - - | head
+case $rc in 0) ;; *) exit $rc;; esac
+timeout -k 10 1100 python -u -m pytest tests -v -m gpu --timeout 600 --timeout-method thread > gpurun_out/pytest_gpu.log 2>&1; rc=$?; echo pytest rc=$rc; grep -E "FAILED|ERROR" gpurun_out/pytest_gpu.log | head -20; tail -3 gpurun_out/pytest_gpu.log
+case $rc in 0|1) ;; *) exit $rc;; esac
+timeout -k 10 600 python bench.py --steps 20 --warmup 3 > gpurun_out/bench.log 2>&1; echo bench rc=$?; tail -c 2500 gpurun_out/bench.log

@@ -16,6 +16,7 @@ import csv
 import glob
 import json
 import os
+import sys
 
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 
@@ -70,6 +71,9 @@ def main():
     if "SQ_WAVES" in sq:
         waves = sq["SQ_WAVES"]["mean"]
         rec["per_wave"] = {n: sq[n]["mean"] / waves for n in sq if n.startswith("SQ_") and n != "SQ_WAVES"}
+    sys.path.insert(0, ROOT)
+    from bench import kernel_sources_sha
+    rec["kernel_sources_sha"] = kernel_sources_sha()
     with open(os.path.join(ROOT, "profiles", "pmc_chol.json"), "w") as fh:
         json.dump(rec, fh, indent=1)
     print(json.dumps(rec, indent=1))
