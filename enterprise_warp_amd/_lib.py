@@ -5,12 +5,20 @@ csrc/Makefile / __graft_entry__.build).  There is no CPU fallback: if the
 library or a GPU is missing, the likelihood raises.  EWARP_HIP_LIB selects
 another build of the same ABI (the dev library libewarp_hip_dev.so with the
 kernel A/B variants and diagnostic exports: scripts/chol_ab.py, gpu_ab tests).
+EWARP_BACKEND=cpu selects the host C++ twin of the same ABI,
+libewarp_cpu.so (csrc/ewarp_cpu.cpp, `make -C enterprise_warp_amd/csrc cpu`):
+an explicit choice for hosts without a GPU, never taken automatically.
 """
 import ctypes as C
 import os
 
 _HERE = os.path.dirname(os.path.abspath(__file__))
-LIB_PATH = os.environ.get("EWARP_HIP_LIB") or os.path.join(_HERE, "libewarp_hip.so")
+CPU_LIB_PATH = os.path.join(_HERE, "libewarp_cpu.so")
+BACKEND = os.environ.get("EWARP_BACKEND", "hip").lower()
+if BACKEND not in ("hip", "cpu"):
+    raise ValueError(f"EWARP_BACKEND={BACKEND!r}: expected 'hip' (default) or 'cpu'")
+LIB_PATH = os.environ.get("EWARP_HIP_LIB") or (CPU_LIB_PATH if BACKEND == "cpu" else
+                                               os.path.join(_HERE, "libewarp_hip.so"))
 DEV_LIB_PATH = os.path.join(_HERE, "libewarp_hip_dev.so")
 
 EWH_ABI_VERSION = 5
@@ -73,10 +81,11 @@ def load():
     # libamdhip64 (same SONAME as /opt/rocm's); if our library is loaded
     # first, torch later maps a second runtime and device queries fail.  Load
     # torch's runtime first so libewarp_hip.so binds to it.
-    try:
-        import torch  # noqa: F401
-    except Exception:  # noqa: BLE001 - torch is optional for the ABI itself
-        pass
+    if BACKEND != "cpu":
+        try:
+            import torch  # noqa: F401
+        except Exception:  # noqa: BLE001 - torch is optional for the ABI itself
+            pass
     if not os.path.exists(LIB_PATH):
         raise EngineError(f"{LIB_PATH} not built: run `make -C enterprise_warp_amd/csrc` or "
                           "__graft_entry__.build(); there is no CPU fallback")

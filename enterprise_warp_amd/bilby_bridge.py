@@ -103,7 +103,8 @@ def get_bilby_prior_dict(pta):
             elif p.type == "truncatednormal":
                 priors[p.name] = _truncnorm(d["mu"], d["sigma"], d["minv"], d["maxv"], p.name)
             else:
-                raise ValueError("Unknown prior type for translation into Bilby. Known types: Normal, Uniform.")
+                raise ValueError(f"{p.name}: scalar prior of type {p.type!r} has no bilby counterpart here "
+                                 f"(supported: uniform, normal, truncatednormal)")
         else:
             if p.name == "jup_orb_elements" and p.type == "uniform":
                 for i in range(p.size):
@@ -112,8 +113,8 @@ def get_bilby_prior_dict(pta):
                 for i in range(p.size):
                     priors[f"{p.name}_{i}"] = _uniform(d["pmin"], d["pmax"], f"{p.name}_{i}")
             else:
-                raise ValueError("Unknown prior with non-unit size for translation into Bilby. "
-                                 "Known prior: jup_orb_elements or tmparams of type Uniform.")
+                raise ValueError(f"{p.name}: vector prior (size {p.size}, type {p.type!r}) has no bilby "
+                                 f"counterpart here (supported: uniform jup_orb_elements / timing-model tmparams)")
     for k in priors:
         if k not in pta.param_names:
             print(f"[!] Warning: Bilby's {k} is not in PTA params")

@@ -1,0 +1,285 @@
+// chol_lat.hip — latency form of the fixed-white-noise factorisation for small
+// batches (one sampler proposal: PTMCMC / bilby call get_lnlikelihood with a
+// single theta, /root/reference/examples/run_example_paramfile.py:27-30,
+// /root/reference/enterprise_warp/bilby_warp.py:35).
+//
+// chol_mfma_kernel gives each (pulsar, sample) unit one wave: at B = 1 the 45
+// units of C3 occupy 45 of 1024 SIMDs and each is a ~20 us chain of 472 MFMAs
+// and 121 dependent pivots on ONE SIMD.  Here each unit gets a 4-wave
+// workgroup (one CU, four SIMDs).  The 16x16 upper blocks (i, j) are dealt to
+// the waves by (i + j) mod 4, which balances every panel's trailing update;
+// the owner of a diagonal block factors it (diag_factor_2l, the same
+// two-level panel as the batched kernel) and publishes E = L^-T and the row
+// scales through LDS; every wave applies them to its blocks of the block row
+// (row_v_2l), publishes those U blocks, and takes its trailing updates
+// A_ij -= U_bi^T U_bj (syrk_update).  The owner of the next diagonal block
+// updates and factors it first (lookahead), so the pivot chain of panel bb+1
+// overlaps the other waves' trailing work of panel bb.
+//
+// Every block sees the same operations in the same order as in
+// chol_mfma_kernel (phi^-1 added at load, updates in panel order, the same
+// panel code), so the factor, the pivots and q are bit-identical; only the
+// log-determinant sum is associated differently (per wave, then across the
+// four waves): strict-equal to the batched kernel, not bit-identical.
+//
+// Sampler I/O is fused in: theta is read straight from the handle's pinned
+// (host-mapped) staging, the last workgroup to finish folds the unit terms
+// over pulsars in pulsar order (the left fold of reduce_units_kernel: the
+// same value the batched path returns) and writes lnL to pinned host memory.
+// One launch per call: no H2D / memset / reduction / D2H operations.
+#include "ewarp_dev.h"
+
+namespace ewh_dev {
+namespace {
+
+constexpr int lat_owner(int i, int j) { return (i + j) & 3; }
+
+template <int NB>
+struct LatLds {
+  double phinv[16 * NB];
+  double phs[16 * NB];
+  double ths[STAGE_THETA_MAX];
+  double E[4][64];          // E = L^-T of the current diagonal block (register r, lane)
+  double R[4][64];          // its row scales D^-1/2 (register r, lane)
+  double U[NB][4][64];      // U blocks (bb, j) of the current block row
+  double ldet[4];
+  int ok[4];
+  double qv;
+  int last;
+};
+
+__device__ __forceinline__ void lds_put(double (*dst)[64], const v4d& v, int lane) {
+  static_for<0, 4>([&](auto R) { dst[decltype(R)::value][lane] = v[decltype(R)::value]; });
+}
+__device__ __forceinline__ v4d lds_get(const double (*src)[64], int lane) {
+  v4d v;
+  static_for<0, 4>([&](auto R) { v[decltype(R)::value] = src[decltype(R)::value][lane]; });
+  return v;
+}
+
+template <int NB, int W>
+__device__ __forceinline__ void lat_wave(LatLds<NB>& S, const CholJob& J, const double* __restrict__ A,
+                                         const double* th, int ldth, int lane, LogAcc& ldet, bool& ok) {
+  constexpr int LD = 16 * NB;
+  const int tid = 64 * W + lane;
+  const int q = lane >> 4, c = lane & 15;
+  // owned blocks, loaded before the prologue (their latency overlaps it)
+  v4d C[NB][NB];
+  static_for<0, NB>([&](auto I) {
+    constexpr int i = decltype(I)::value;
+    static_for<i, NB>([&](auto JJ) {
+      constexpr int j = decltype(JJ)::value;
+      if constexpr (lat_owner(i, j) == W) {
+        static_for<0, 4>([&](auto R) {
+          constexpr int r = decltype(R)::value;
+          C[i][j][r] = A[(long long)(16 * i + q + 4 * r) * LD + 16 * j + c];
+        });
+      }
+    });
+  });
+  // ---- prologue: phi^-1 of every column (the arithmetic of chol_mfma_kernel) ----
+  const bool stage = ldth <= STAGE_THETA_MAX;
+  if (stage) {
+    for (int i = tid; i < ldth; i += 256) S.ths[i] = th[i];
+    __syncthreads();
+  }
+  const double* tp = stage ? S.ths : th;
+  if (J.urec != nullptr) {
+    for (int u = tid; u < J.nu; u += 256) {
+      const URec& R = J.urec[u];
+      double ph = 0.0;
+      for (int e = 0; e < R.ne; ++e) ph += spec_phi_body(R.e[e], tp);
+      S.phs[u] = ph;
+    }
+    __syncthreads();
+    for (int a = tid; a < LD; a += 256) {
+      const int ur = a < J.mreal ? J.urep[a] : -1;
+      double pi = 0.0;
+      if (ur >= 0) {
+        const double ph = S.phs[ur];
+        pi = 1.0 / ph;
+        ldet.add(ph);
+      }
+      S.phinv[a] = pi;
+    }
+  } else {
+    const bool dedup = J.rep != nullptr;
+    if (dedup) {
+      for (int i = tid; i < J.nu; i += 256) {
+        const int a = J.ulist[i];
+        double ph = 0.0;
+        for (int e = J.col_ptr[a]; e < J.col_ptr[a + 1]; ++e) ph += spec_phi_body(J.spec[e], tp);
+        S.phs[a] = ph;
+      }
+    }
+    __syncthreads();
+    for (int a = tid; a < LD; a += 256) {
+      double pi = 0.0;
+      if (a < J.mreal && J.col_ptr[a] < J.col_ptr[a + 1]) {
+        double ph = 0.0;
+        if (dedup) {
+          ph = S.phs[J.rep[a]];
+        } else {
+          for (int e = J.col_ptr[a]; e < J.col_ptr[a + 1]; ++e) ph += spec_phi_body(J.spec[e], tp);
+        }
+        pi = 1.0 / ph;
+        ldet.add(ph);
+      }
+      S.phinv[a] = pi;
+    }
+  }
+  __syncthreads();
+  static_for<0, NB>([&](auto I) {
+    constexpr int i = decltype(I)::value;
+    if constexpr (lat_owner(i, i) == W) {
+      const double pd = S.phinv[16 * i + c];
+      static_for<0, 4>([&](auto R) {
+        constexpr int r = decltype(R)::value;
+        C[i][i][r] += (q + 4 * r == c) ? pd : 0.0;
+      });
+    }
+  });
+  const int klast = __builtin_amdgcn_readfirstlane(J.mreal - 16 * (NB - 1));
+  v4d E;
+  double rsr[4];
+  // factor diagonal block BB (owner only); publish E and the scales, or q
+  auto factor = [&](auto BBc) {
+    constexpr int bb = decltype(BBc)::value;
+    diag_factor_2l<NB, bb, true>(C[bb][bb], E, rsr, q, c, ldet, ok, klast);
+    if constexpr (bb < NB - 1) {
+      lds_put(S.E, E, lane);
+      static_for<0, 4>([&](auto R) { S.R[decltype(R)::value][lane] = rsr[decltype(R)::value]; });
+    } else {
+      const double qv = readlane_d(C[bb][bb][3], 63);
+      if (lane == 0) S.qv = qv;
+    }
+  };
+  if constexpr (lat_owner(0, 0) == W) factor(std::integral_constant<int, 0>{});
+  static_for<0, NB - 1>([&](auto BBc) {
+    constexpr int bb = decltype(BBc)::value;
+    __syncthreads();                                       // E, scales of panel bb
+    constexpr bool row_owned = [] {
+      for (int j = bb + 1; j < NB; ++j)
+        if (lat_owner(bb, j) == W) return true;
+      return false;
+    }();
+    if constexpr (row_owned) {
+      if constexpr (lat_owner(bb, bb) != W) {
+        E = lds_get(S.E, lane);
+        static_for<0, 4>([&](auto R) { rsr[decltype(R)::value] = S.R[decltype(R)::value][lane]; });
+      }
+      static_for<bb + 1, NB>([&](auto JJ) {
+        constexpr int j = decltype(JJ)::value;
+        if constexpr (lat_owner(bb, j) == W) row_v_2l(E, C[bb][j]);
+      });
+      static_for<bb + 1, NB>([&](auto JJ) {
+        constexpr int j = decltype(JJ)::value;
+        if constexpr (lat_owner(bb, j) == W) {
+          static_for<0, 4>([&](auto R) { C[bb][j][decltype(R)::value] *= rsr[decltype(R)::value]; });
+          lds_put(S.U[j], C[bb][j], lane);
+        }
+      });
+    }
+    __syncthreads();                                       // U blocks of row bb
+    auto ublk = [&](auto II) -> v4d {
+      constexpr int i = decltype(II)::value;
+      if constexpr (lat_owner(bb, i) == W) return C[bb][i];
+      else return lds_get(S.U[i], lane);
+    };
+    // lookahead: the next diagonal block first, then its panel
+    if constexpr (lat_owner(bb + 1, bb + 1) == W) {
+      const v4d u = ublk(std::integral_constant<int, bb + 1>{});
+      syrk_update(C[bb + 1][bb + 1], u, u);
+      factor(std::integral_constant<int, bb + 1>{});
+    }
+    static_for<bb + 1, NB>([&](auto II) {
+      constexpr int i = decltype(II)::value;
+      constexpr bool any = [] {
+        for (int j = i; j < NB; ++j)
+          if (lat_owner(i, j) == W && !(i == bb + 1 && j == bb + 1)) return true;
+        return false;
+      }();
+      if constexpr (any) {
+        const v4d ui = ublk(II);
+        static_for<i, NB>([&](auto JJ) {
+          constexpr int j = decltype(JJ)::value;
+          if constexpr (lat_owner(i, j) == W && !(i == bb + 1 && j == bb + 1)) {
+            if constexpr (j == i) syrk_update(C[i][j], ui, ui);
+            else syrk_update(C[i][j], ui, ublk(JJ));
+          }
+        });
+      }
+    });
+  });
+}
+
+template <int NB>
+__global__ __launch_bounds__(256) void chol_lat_kernel(const CholJob* __restrict__ jobs, int B, int P,
+                                                       const double* theta, int ldth, double* __restrict__ out_units,
+                                                       double* out, unsigned* counter) {
+  __shared__ LatLds<NB> S;
+  const int tid = threadIdx.x, w = tid >> 6, lane = tid & 63;
+  const int u = blockIdx.x;
+  const int p = u / B, b = u % B;
+  const CholJob J = jobs[p];
+  const double* A = J.mats + (long long)b * J.mstride;
+  const double* th = theta + (long long)b * ldth;
+  LogAcc ldet;
+  bool ok = true;
+  switch (w) {
+    case 0: lat_wave<NB, 0>(S, J, A, th, ldth, lane, ldet, ok); break;
+    case 1: lat_wave<NB, 1>(S, J, A, th, ldth, lane, ldet, ok); break;
+    case 2: lat_wave<NB, 2>(S, J, A, th, ldth, lane, ldet, ok); break;
+    default: lat_wave<NB, 3>(S, J, A, th, ldth, lane, ldet, ok); break;
+  }
+  const double lw = wave_sum(ldet.value());
+  const bool okw = __all(ok);
+  if (lane == 0) {
+    S.ldet[w] = lw;
+    S.ok[w] = okw ? 1 : 0;
+  }
+  __syncthreads();
+  if (tid == 0) {
+    double lnl = J.K[(long long)b * J.kstride] - 0.5 * S.qv - 0.5 * (((S.ldet[0] + S.ldet[1]) + S.ldet[2]) + S.ldet[3]);
+    if (!(S.ok[0] && S.ok[1] && S.ok[2] && S.ok[3]) || J.fail) lnl = -INFINITY;
+    __hip_atomic_store(out_units + (long long)p * B + b, lnl, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    __threadfence();
+    const unsigned t = __hip_atomic_fetch_add(counter, 1u, __ATOMIC_ACQ_REL, __HIP_MEMORY_SCOPE_AGENT);
+    S.last = t == gridDim.x - 1;
+  }
+  __syncthreads();
+  if (S.last) {
+    // the last unit to finish: lnL_b = sum over pulsars in pulsar order
+    __threadfence();
+    for (int bq = tid; bq < B; bq += 256) {
+      double s = 0.0;
+      for (int pp = 0; pp < P; ++pp)
+        s += __hip_atomic_load(out_units + (long long)pp * B + bq, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      out[bq] = s;
+    }
+    __threadfence_system();
+    if (tid == 0) __hip_atomic_store(counter, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  }
+}
+
+}  // namespace
+
+int launch_chol_lat(int nb, const CholJob* jobs, int B, int P, const double* theta, int ldth, double* units,
+                    double* out, unsigned* counter, hipStream_t st) {
+  const dim3 grid((unsigned)(P * B)), block(256);
+  switch (nb) {
+    case 1: hipLaunchKernelGGL(chol_lat_kernel<1>, grid, block, 0, st, jobs, B, P, theta, ldth, units, out, counter); break;
+    case 2: hipLaunchKernelGGL(chol_lat_kernel<2>, grid, block, 0, st, jobs, B, P, theta, ldth, units, out, counter); break;
+    case 3: hipLaunchKernelGGL(chol_lat_kernel<3>, grid, block, 0, st, jobs, B, P, theta, ldth, units, out, counter); break;
+    case 4: hipLaunchKernelGGL(chol_lat_kernel<4>, grid, block, 0, st, jobs, B, P, theta, ldth, units, out, counter); break;
+    case 5: hipLaunchKernelGGL(chol_lat_kernel<5>, grid, block, 0, st, jobs, B, P, theta, ldth, units, out, counter); break;
+    case 6: hipLaunchKernelGGL(chol_lat_kernel<6>, grid, block, 0, st, jobs, B, P, theta, ldth, units, out, counter); break;
+    case 7: hipLaunchKernelGGL(chol_lat_kernel<7>, grid, block, 0, st, jobs, B, P, theta, ldth, units, out, counter); break;
+    case 8: hipLaunchKernelGGL(chol_lat_kernel<8>, grid, block, 0, st, jobs, B, P, theta, ldth, units, out, counter); break;
+    default: return 1;
+  }
+  const hipError_t e = hipGetLastError();
+  return e == hipSuccess ? 0 : set_err(EWH_E_HIP, std::string("chol_lat_kernel: ") + hipGetErrorString(e));
+}
+
+}  // namespace ewh_dev

@@ -686,24 +686,81 @@ struct NoHook {
   __device__ __forceinline__ void on_scale(int, double) const {}
 };
 
-// Panel forms (template ALG of panel_ldl_row / chol_mfma_kernel):
-//  PANEL_2L (25, the default): two-level.  The 16 pivots of the diagonal
-//    block run in four sub-panels of 4 rows -- register s of the C/D layout.
-//    Inside a sub-panel the pivots update only register s (rows q > kq) and
-//    E; after it, the sub-panel's rows are scaled to U_s = D_s^-1/2 V_s and
-//    the rows below take D -= U_s^T U_s by ONE MFMA (the 16x16x4 shape is
-//    exactly a 4-row rank update).  That update is symmetric by
-//    construction, so the multipliers read from the lower triangle
-//    (A[i][k], i > k) stay equal to the upper entries they stand for.
-//  PANEL_1L (11, dev A/B only: the round-2 default): every pivot updates
-//    every register r >= kr by VALU.  The update A[i][c] -= A[i][k] (A[k][c] /
-//    d) rounds differently from its mirror A[c][i] -= A[c][k] (A[k][i] / d),
-//    so the lower triangle drifts from the upper one and, on ill-conditioned
-//    draws, the Schur complements drift with it (tests/golden: c1_turnover
-//    sample 0 at 4e3x the strict bound vs 22x for PANEL_2L and 79x for
-//    enterprise's LAPACK order).
-constexpr int PANEL_1L = 11;
-constexpr int PANEL_2L = 25;
+
+// PANEL_2L on the diagonal block D of block row BB (of NB): its 16 pivots in
+// four sub-panels of 4 rows (register s of the C/D layout).  Inside a
+// sub-panel the pivots update only register s (rows q > kq) and E; after it,
+// the sub-panel's rows are scaled to U_s = D_s^-1/2 V_s and the rows below
+// take D -= U_s^T U_s by ONE MFMA.  Leaves E = L^-T (column operations) and
+// the row scales rsr[r] = D^-1/2 of register r; accumulates log d_k (lane
+// c == 0 of each row) and d_k > 0.  RL: the last column of block row NB-1 is
+// the residual (not pivoted); klim: pivots >= klim of that block row are pads
+// (identity rows and columns: pivot 1, every multiplier 0) and are skipped.
+template <int NB, int BB, bool RL>
+__device__ __forceinline__ void diag_factor_2l(v4d& D, v4d& E, double (&rsr)[4], int q, int c, LogAcc& ldet,
+                                               bool& ok, int klim) {
+  constexpr bool LASTR = RL && BB == NB - 1;          // block row holding the residual
+  static_for<0, 4>([&](auto R) {
+    constexpr int r = decltype(R)::value;
+    E[r] = (q + 4 * r == c) ? 1.0 : 0.0;
+    rsr[r] = 1.0;
+  });
+  // (Folding the row scales into E's columns instead -- E D^-1/2, one gather,
+  // four multiplies -- was tried in round 3: the wide chol_big_kernel and the
+  // one-wave NB = 9 kernel then faulted with an illegal address on the GPU;
+  // not kept.)
+  static_for<0, 4>([&](auto KR) {
+    constexpr int kr = decltype(KR)::value;
+    constexpr int nk = (LASTR && kr == 3) ? 3 : 4;   // the r column is not pivoted
+    static_for<0, nk>([&](auto KQc) {
+      constexpr int kq = decltype(KQc)::value;
+      constexpr int k = 4 * kr + kq;
+      if constexpr (LASTR) {
+        if (k >= klim) return;                         // wave-uniform: pad pivots
+      }
+      constexpr bool doe = !LASTR && k < 15;
+      const double xk = __shfl(D[kr], 16 * kq + c);    // A[k][c]
+      const double d = readlane_d(D[kr], 16 * kq + k);
+      const double nw = div_fast(-xk, d);
+      const double nwm = (doe && c > k) ? nw : 0.0;
+      pivot_fused<k, kr, kq, doe, kq == 0, false>(D, E, nw, nwm);
+    });
+    // sub-panel kr done: lane (q, c) takes the pivot of row 4 kr + q (lane
+    // (q, 4 kr + q)): log-det, positivity, row scale; U_s = D_s^-1/2 V_s and
+    // the rows below take D -= U_s^T U_s (one MFMA, in place: registers
+    // <= kr are not read again)
+    auto sub = [&]() {
+      const double dg = __shfl(D[kr], 17 * q + 4 * kr);
+      const double dv = (LASTR && kr == 3 && q == 3) ? 1.0 : dg;   // (the r row)
+      ok = ok && (dv > 0.0);
+      if (c == 0) ldet.add(dv);
+      if constexpr (!(LASTR && kr == 3)) {
+        const double rs = rsqrt_fast(dv);
+        rsr[kr] = rs;
+        if constexpr (kr < 3) {
+          const double u = D[kr] * rs;
+          D = __builtin_amdgcn_mfma_f64_16x16x4f64(u, u, D, 0, 0, 1);
+        }
+      }
+    };
+    if constexpr (LASTR) {
+      if (4 * kr < klim) sub();                      // (a sub-panel of pads: pivots 1, no update)
+    } else {
+      sub();
+    }
+  });
+}
+
+// The rest of a block row after its diagonal block: V = E^T A (4 MFMAs)
+// (row_v_2l), rows scaled to U = D^-1/2 V (row r of register r times rsr[r]).
+__device__ __forceinline__ void row_v_2l(const v4d& E, v4d& A) {
+  v4d acc = {0.0, 0.0, 0.0, 0.0};
+  static_for<0, 4>([&](auto S) {
+    constexpr int s = decltype(S)::value;
+    acc = __builtin_amdgcn_mfma_f64_16x16x4f64(E[s], A[s], acc, 0, 0, 0);
+  });
+  A = acc;
+}
 
 // The LDL^T panel of block row BB over the blocks blk(j), j = BB..NB-1 (C/D
 // layout, upper triangle; the diagonal block is held in full): eliminates
@@ -715,30 +772,47 @@ constexpr int PANEL_2L = 25;
 // RL: the last column of block row NB-1 is the residual (not pivoted), as in
 // the per-pulsar factorisations; false for a plain SPD block (the dense
 // cross-pulsar factorisation's diagonal tiles).
+// PANEL_2L (the default): diag_factor_2l + row_v_2l + the row scales.  PANEL_1L (dev A/B
+// only: the round-2 default): every pivot updates every register r >= kr by
+// VALU.  The update A[i][c] -= A[i][k] (A[k][c] / d) rounds differently from
+// its mirror A[c][i] -= A[c][k] (A[k][i] / d), so the lower triangle drifts
+// from the upper one and, on ill-conditioned draws, the Schur complements
+// drift with it (tests/golden: c1_turnover sample 0 at 4e3x the strict bound
+// vs 22x for PANEL_2L and 79x for enterprise's LAPACK order).
 // PACK (PANEL_1L): the row scales D^-1/2 of all 16 rows by one gather + one
 // rsqrt per lane (lane (q, c) takes d of row q + 4 (c/4)); else one per
 // register (the phase-1 form of chol_mfma_kernel<8>, where the packed
-// temporaries spill).  PANEL_2L forms each sub-panel's scales when it closes.
-// klim: pivots >= klim of the last block row are pads (identity rows and
-// columns: pivot 1, every multiplier 0) and are skipped (bit-identical).
+// temporaries spill).
+// klim: pivots >= klim of the last block row are pads and are skipped.
+constexpr int PANEL_1L = 11;
+constexpr int PANEL_2L = 25;
+
 template <int NB, int ALG, bool RL, bool PACK, typename BBt, typename Blk, typename Hook = NoHook>
 __device__ __forceinline__ void panel_ldl_row(BBt BBc, Blk&& blk, int q, int c, LogAcc& ldet, bool& ok,
                                               const Hook& hook = Hook{}, int klim = 16) {
   constexpr int bb = decltype(BBc)::value;
-  constexpr bool TWO = ALG == PANEL_2L;
-  static_assert(ALG == PANEL_1L || TWO, "unknown panel form");
+  static_assert(ALG == PANEL_1L || ALG == PANEL_2L, "unknown panel form");
   constexpr bool LASTR = RL && bb == NB - 1;          // block row holding the residual
+  if constexpr (ALG == PANEL_2L) {
+    v4d E;
+    double rsr[4];
+    diag_factor_2l<NB, bb, RL>(blk(BBc), E, rsr, q, c, ldet, ok, klim);
+    if constexpr (!LASTR) {
+      hook.on_e(E);
+      static_for<bb + 1, NB>([&](auto JJ) { row_v_2l(E, blk(JJ)); });
+      static_for<0, 4>([&](auto R) {
+        constexpr int r = decltype(R)::value;
+        hook.on_scale(r, rsr[r]);
+        static_for<bb + 1, NB>([&](auto JJ) { blk(JJ)[r] *= rsr[r]; });
+      });
+    }
+    return;
+  } else {
   v4d E;
   static_for<0, 4>([&](auto R) {
     constexpr int r = decltype(R)::value;
     E[r] = (q + 4 * r == c) ? 1.0 : 0.0;
   });
-  // two-level: the row scales D^-1/2 of sub-panel s, formed when it closes.
-  // (Folding them into E's columns instead -- E D^-1/2, one gather, four
-  // multiplies -- was tried in round 3: the wide chol_big_kernel and the
-  // one-wave NB = 9 kernel then faulted with an illegal address on the GPU;
-  // not kept.)
-  double rsr[4] = {1.0, 1.0, 1.0, 1.0};
   static_for<0, 4>([&](auto KR) {
     constexpr int kr = decltype(KR)::value;
     constexpr int nk = (LASTR && kr == 3) ? 3 : 4;   // the r column is not pivoted
@@ -753,33 +827,8 @@ __device__ __forceinline__ void panel_ldl_row(BBt BBc, Blk&& blk, int q, int c, 
       const double d = readlane_d(blk(BBc)[kr], 16 * kq + k);
       const double nw = div_fast(-xk, d);
       const double nwm = (doe && c > k) ? nw : 0.0;
-      pivot_fused<k, kr, kq, doe, (TWO ? kq == 0 : k == 0), !TWO>(blk(BBc), E, nw, nwm);
+      pivot_fused<k, kr, kq, doe, k == 0, true>(blk(BBc), E, nw, nwm);
     });
-    if constexpr (TWO) {
-      // sub-panel kr done: lane (q, c) takes the pivot of row 4 kr + q (lane
-      // (q, 4 kr + q)): log-det, positivity, row scale; U_s = D_s^-1/2 V_s and
-      // the rows below take D -= U_s^T U_s (one MFMA, in place: registers
-      // <= kr are not read again)
-      auto sub = [&]() {
-        const double dg = __shfl(blk(BBc)[kr], 17 * q + 4 * kr);
-        const double dv = (LASTR && kr == 3 && q == 3) ? 1.0 : dg;   // (the r row)
-        ok = ok && (dv > 0.0);
-        if (c == 0) ldet.add(dv);
-        if constexpr (!(LASTR && kr == 3)) {
-          const double rs = rsqrt_fast(dv);
-          rsr[kr] = rs;
-          if constexpr (kr < 3) {
-            const double u = blk(BBc)[kr] * rs;
-            blk(BBc) = __builtin_amdgcn_mfma_f64_16x16x4f64(u, u, blk(BBc), 0, 0, 1);
-          }
-        }
-      };
-      if constexpr (LASTR) {
-        if (4 * kr < klim) sub();                      // (a sub-panel of pads: pivots 1, no update)
-      } else {
-        sub();
-      }
-    }
   });
   if constexpr (!LASTR) hook.on_e(E);
   static_for<bb + 1, NB>([&](auto JJ) {
@@ -792,15 +841,7 @@ __device__ __forceinline__ void panel_ldl_row(BBt BBc, Blk&& blk, int q, int c, 
   });
   // rows of the block row -> U = d^-1/2 V (the diagonal block itself is not
   // needed after its panel; the last block row has nothing to scale)
-  if constexpr (TWO) {
-    if constexpr (!LASTR) {
-      static_for<0, 4>([&](auto R) {
-        constexpr int r = decltype(R)::value;
-        hook.on_scale(r, rsr[r]);
-        static_for<bb + 1, NB>([&](auto JJ) { blk(JJ)[r] *= rsr[r]; });
-      });
-    }
-  } else if constexpr (PACK) {
+  if constexpr (PACK) {
     // d of row q + 4r read from the diagonal (lane 17q + 4r); lane (q, c)
     // takes d of row q + 4 (c/4) -- held in register c/4 of lane
     // (q, q + 4 (c/4)), whose own c/4 is the same -- so one gather, one rsqrt
@@ -835,6 +876,7 @@ __device__ __forceinline__ void panel_ldl_row(BBt BBc, Blk&& blk, int q, int c, 
         static_for<bb + 1, NB>([&](auto JJ) { blk(JJ)[r] *= rs; });
       }
     });
+  }
   }
 }
 
@@ -1223,6 +1265,13 @@ int launch_chol_small(int mode, int nb, const CholJob* jobs, int B, long long u0
                       const double* theta, int ldth, double* units, hipStream_t st);
 int launch_chol_big_nb(int nb, const CholJob* jobs, int B, long long u0, long long n, int b_off,
                        const double* theta, int ldth, double* units, double* scr, long long cap, hipStream_t st);
+// latency form for small batches (chol_lat.hip): one 4-wave workgroup per
+// unit of units [0, P B); theta and out may be host-mapped pinned memory; the
+// last workgroup folds the unit terms into out[B] and re-zeroes *counter.
+// Returns 1 if nb has no latency kernel (caller uses the batched path).
+constexpr int LAT_NB_MAX = 8;
+int launch_chol_lat(int nb, const CholJob* jobs, int B, int P, const double* theta, int ldth, double* units,
+                    double* out, unsigned* counter, hipStream_t st);
 // keep_out: pulsar-major kept blocks, keep_bs samples per pulsar (see chol_mfma_kernel KEEP)
 int launch_partial_nb(int nb, int keep, const CholJob* jobs, int B, long long u0, long long n,
                       const double* theta, int ldth, double* units, double* keep_out, int keep_bs, hipStream_t st);

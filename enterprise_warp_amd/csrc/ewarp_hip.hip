@@ -25,6 +25,7 @@
 //    v_mfma_f64_16x16x4_f64), chol_lds (general fallback, matrix in LDS),
 //    reduce_units (sum over pulsars in pulsar order).
 #include "ewarp_dev.h"
+#include "ewarp_desc.h"
 
 #include <map>
 
@@ -396,6 +397,8 @@ __global__ __launch_bounds__(256) void common_minv_kernel(const CommonPsr* __res
 // its elements in place -- no integer division or LDS round trip per element
 // (the LDS version above costs ~30x more on C5's 100 x 100 blocks).
 constexpr int MINV_PMAX = 128;
+// sample chunks up to this size factor Sigma_c right-looking (corr_finish)
+constexpr int CORR_RIGHT_LOOKING_MAX = 4;
 
 __global__ __launch_bounds__(256) void common_minv_reg_kernel(const CommonPsr* __restrict__ cps, int P,
                                                               const double* __restrict__ orf,
@@ -1194,6 +1197,11 @@ struct DevCtx {
   };
   std::vector<Graph> graphs;
   long long graph_clock = 0;
+  // latency path of small single-device batches (chol_lat.hip): every pulsar
+  // has the same reduced block count lat_nb <= LAT_NB_MAX (0: not eligible);
+  // lat_ctr = the kernel's finished-unit counter (zero between calls)
+  int lat_nb = 0;
+  unsigned* d_lat_ctr = nullptr;
 };
 
 namespace {
@@ -1233,72 +1241,9 @@ size_t lds_bytes_chol(int mreal) {
 bool pref_uses_theta(const ewh_pref& r) { return r.idx >= 0; }
 
 int validate(const ewh_pta_desc* d) {
-  if (!d || d->abi_version != EWH_ABI_VERSION) return set_err(EWH_E_INVALID, "bad descriptor / ABI version");
-  if (d->n_pulsar <= 0 || !d->pulsars) return set_err(EWH_E_INVALID, "no pulsars");
-  if (d->n_param < 0) return set_err(EWH_E_INVALID, "n_param < 0");
-  for (int p = 0; p < d->n_pulsar; ++p) {
-    const ewh_pulsar_desc& s = d->pulsars[p];
-    const std::string tag = "pulsar " + std::to_string(p) + ": ";
-    if (s.n_toa <= 0 || s.n_col < 0 || s.n_lead_const < 0 || s.n_lead_const > s.n_col)
-      return set_err(EWH_E_INVALID, tag + "bad sizes");
-    if ((s.n_col && !s.basis) || !s.resid || !s.toaerr || !s.efac_slot || !s.equad_slot ||
-        (s.n_slot && !s.slots) || (s.n_spec && !s.spec))
-      return set_err(EWH_E_INVALID, tag + "null pointer");
-    if (s.n_epoch && (!s.epoch_start || !s.epoch_stop || !s.epoch_slot))
-      return set_err(EWH_E_INVALID, tag + "null epoch pointer");
-    for (int i = 0; i < s.n_slot; ++i)
-      if (s.slots[i].idx >= d->n_param) return set_err(EWH_E_INVALID, tag + "slot theta index out of range");
-    for (int t = 0; t < s.n_toa; ++t) {
-      if (s.efac_slot[t] < 0 || s.efac_slot[t] >= s.n_slot) return set_err(EWH_E_INVALID, tag + "efac slot out of range");
-      if (s.equad_slot[t] >= s.n_slot) return set_err(EWH_E_INVALID, tag + "equad slot out of range");
-    }
-    int prev = 0;
-    for (int e = 0; e < s.n_epoch; ++e) {
-      if (s.epoch_start[e] < prev || s.epoch_stop[e] <= s.epoch_start[e] + 1 || s.epoch_stop[e] > s.n_toa)
-        return set_err(EWH_E_INVALID, tag + "epochs must be ordered, disjoint slices of >= 2 TOAs");
-      if (s.epoch_slot[e] < 0 || s.epoch_slot[e] >= s.n_slot) return set_err(EWH_E_INVALID, tag + "epoch slot out of range");
-      prev = s.epoch_stop[e];
-    }
-    if (s.n_bgroup < 0 || (s.n_bgroup > 0 && (!s.bgroup_idx || !s.col_bgroup || !s.ln_chrom)))
-      return set_err(EWH_E_INVALID, tag + "bad basis-group tables");
-    for (int g = 0; g < s.n_bgroup; ++g)
-      if (s.bgroup_idx[g].idx >= d->n_param) return set_err(EWH_E_INVALID, tag + "basis-group theta index out of range");
-    for (int j = 0; s.n_bgroup > 0 && j < s.n_col; ++j)
-      if (s.col_bgroup[j] < -1 || s.col_bgroup[j] >= s.n_bgroup || (j < s.n_lead_const && s.col_bgroup[j] >= 0))
-        return set_err(EWH_E_INVALID, tag + "bad column basis group");
-    std::vector<int> cnt(s.n_col, 0);
-    for (int e = 0; e < s.n_spec; ++e) {
-      const ewh_spec_entry& sp = s.spec[e];
-      if (sp.col < 0 || sp.col >= s.n_col) return set_err(EWH_E_INVALID, tag + "spectral column out of range");
-      if (sp.kind < EWH_SPEC_POWERLAW || sp.kind > EWH_SPEC_CONST) return set_err(EWH_E_INVALID, tag + "bad spectral kind");
-      if (sp.p0.idx >= d->n_param || sp.p1.idx >= d->n_param || sp.p2.idx >= d->n_param)
-        return set_err(EWH_E_INVALID, tag + "spectral theta index out of range");
-      if (sp.col < s.n_lead_const && sp.kind != EWH_SPEC_CONST)
-        return set_err(EWH_E_INVALID, tag + "leading columns must have constant phi");
-      cnt[sp.col]++;
-    }
-    const int ncom = d->common ? s.n_common : 0;
-    if (d->common && (s.n_common != d->common->n_col || s.n_common > s.n_col - s.n_lead_const))
-      return set_err(EWH_E_INVALID, tag + "n_common must equal common->n_col and follow the leading columns");
-    if (!d->common && s.n_common != 0) return set_err(EWH_E_INVALID, tag + "n_common without a common descriptor");
-    for (int j = 0; j < s.n_col - ncom; ++j)
-      if (!cnt[j]) return set_err(EWH_E_INVALID, tag + "column " + std::to_string(j) + " has no phi entry");
-  }
-  if (d->common) {
-    const ewh_common_desc& c = *d->common;
-    if (c.kind != EWH_COMMON_CORRELATED && c.kind != EWH_COMMON_OPTSTAT)
-      return set_err(EWH_E_INVALID, "common: bad kind");
-    if (c.n_col < 1 || c.n_col > 31 || !c.orf || (c.kind == EWH_COMMON_CORRELATED && !c.spec))
-      return set_err(EWH_E_INVALID, "common: need 1..31 columns, an ORF matrix and spectral entries");
-    if (d->n_pulsar > 128) return set_err(EWH_E_UNSUPPORTED, "common: at most 128 pulsars");
-    for (int g = 0; c.kind == EWH_COMMON_CORRELATED && g < c.n_col; ++g) {
-      const ewh_spec_entry& sp = c.spec[g];
-      if (sp.col != g || sp.kind < EWH_SPEC_POWERLAW || sp.kind > EWH_SPEC_CONST || sp.p0.idx >= d->n_param ||
-          sp.p1.idx >= d->n_param || sp.p2.idx >= d->n_param)
-        return set_err(EWH_E_INVALID, "common: bad spectral entry " + std::to_string(g));
-    }
-  }
-  return 0;
+  std::string msg;
+  const int rc = ewh_desc::desc_check(d, msg);
+  return rc ? set_err(rc, msg) : 0;
 }
 
 DSpec to_dspec(const ewh_spec_entry& e, int col) {
@@ -1721,12 +1666,31 @@ int corr_finish(DevCtx* h, const double* theta_dev, int B, const double* keep, d
     EWH_HIP(hipMemsetAsync(h->d_cldet, 0, sizeof(double) * nb, st));
     EWH_HIP(hipMemsetAsync(h->d_cq, 0, sizeof(double) * nb, st));
     EWH_HIP(hipMemsetAsync(h->d_cfail, 0, sizeof(int) * nb, st));
+    // one or a few proposals (PTMCMC): right-looking -- after each panel the
+    // trailing tiles (i, j > k) are updated in parallel (m (m + 1) / 2 tiles
+    // per launch, K = 64), instead of the left-looking row update whose
+    // K = 64 k accumulation of one tile is a serial chain on one CU.  Tile
+    // (i, j) takes the same K = 64 slabs in the same order into the same
+    // accumulator (stored and reloaded in full between panels): bit-identical.
+    const bool right = h->kernel_mode == 0 && nb <= CORR_RIGHT_LOOKING_MAX;
     for (int k = 0; k < nbk; ++k) {
       const int m = nbk - k - 1;
+      if (right) {
+        if (m == 0) {
+          hipLaunchKernelGGL(HIP_KERNEL_NAME(dchol_diag_reg_kernel<true>), dim3(nb), dim3(64), 0, st, h->d_dense,
+                             h->Np, k, h->d_wbuf, h->d_cldet, h->d_cq, h->d_cfail);
+          continue;
+        }
+        hipLaunchKernelGGL(HIP_KERNEL_NAME(dchol_diag_reg_kernel<false>), dim3(nb), dim3(64), 0, st, h->d_dense,
+                           h->Np, k, h->d_wbuf, h->d_cldet, h->d_cq, h->d_cfail);
+        hipLaunchKernelGGL(dchol_panel_reg_kernel, dim3(4 * m, nb), dim3(64), 0, st, h->d_dense, h->Np, k, h->d_wbuf);
+        hipLaunchKernelGGL(dchol_update_kernel, dim3(m * (m + 1) / 2, nb), dim3(256), 0, st, h->d_dense, h->Np, k);
+        continue;
+      }
       // default for large sample chunks: row update + panel fused (the updated
-      // tile never round-trips through HBM); small chunks (one PTMCMC
-      // proposal) keep the row update of every tile in one launch, which
-      // shortens the dependent chain per block row
+      // tile never round-trips through HBM); small chunks keep the row update
+      // of every tile in one launch, which shortens the dependent chain per
+      // block row
       const bool fused = h->kernel_mode != 1 && h->kernel_mode != 7 && nb >= 64;
       if (h->kernel_mode == 1 && k > 0)     // round-1 row update (both operands staged through LDS)
         hipLaunchKernelGGL(dchol_rowupdate_kernel, dim3(m + 1, nb), dim3(256), 0, st, h->d_dense, h->Np, k);
@@ -2010,6 +1974,16 @@ int create_ctx(const ewh_pta_desc* d, const std::vector<ProjCoef>& proj, int dev
     return bail(set_err(EWH_E_UNSUPPORTED, "correlated common process: white noise must be fixed (TNT cached)"));
   if (h->white_fixed && (rc = setup_fixed(h))) return bail(rc);
   if (d->common && (rc = setup_common(h, d))) return bail(rc);
+  if (h->white_fixed && !h->corr && !h->osmode) {
+    int nb = h->psr[0].fx_nb;
+    for (const auto& ps : h->psr)
+      if (ps.fx_nb != nb) nb = 0;
+    if (nb >= 1 && nb <= LAT_NB_MAX) {
+      if ((rc = dalloc(h, &h->d_lat_ctr, 1))) return bail(rc);
+      EWH_HIP(hipMemset(h->d_lat_ctr, 0, sizeof(unsigned)));
+      h->lat_nb = nb;
+    }
+  }
   *out = h;
   return 0;
 }
@@ -2243,7 +2217,8 @@ int ensure_pinned(double** p, size_t* cap, size_t need) {
   if (*p) (void)hipHostFree(*p);
   *p = nullptr;
   *cap = 0;
-  hipError_t e = hipHostMalloc((void**)p, std::max<size_t>(need, 1) * sizeof(double), hipHostMallocPortable);
+  hipError_t e = hipHostMalloc((void**)p, std::max<size_t>(need, 1) * sizeof(double),
+                               hipHostMallocPortable | hipHostMallocMapped);
   if (e != hipSuccess) return set_err(EWH_E_NOMEM, std::string("hipHostMalloc: ") + hipGetErrorString(e));
   *cap = need;
   return 0;
@@ -2331,10 +2306,31 @@ int lnl_batch_corr_pulsars(ewh_handle* H, int B, double* out_host) {
 // One device: replay the captured graph of this batch size when there is one;
 // otherwise run the batch eagerly (that also sizes every scratch buffer) and
 // capture the same sequence for the next call.
+constexpr int LAT_B_MAX = 16;   // batches up to this size take the latency kernel
+
 int lnl_batch_single(ewh_handle* H, DevCtx* h, int B, double* out_host) {
   int rc;
   EWH_HIP(hipSetDevice(h->device));
   if ((rc = ensure_pinned(&H->h_out, &H->h_out_cap, (size_t)B))) return rc;
+  if (h->lat_nb > 0 && B <= LAT_B_MAX && h->kernel_mode == 0) {
+    // latency path: one launch reads theta from the pinned staging, folds
+    // the unit terms and writes lnL to pinned memory (chol_lat.hip)
+    if ((rc = ensure_units(h, B))) return rc;
+    double *th_dev = nullptr, *out_dev = nullptr;
+    EWH_HIP(hipHostGetDevicePointer((void**)&th_dev, H->h_theta, 0));
+    EWH_HIP(hipHostGetDevicePointer((void**)&out_dev, H->h_out, 0));
+    if ((rc = launch_chol_lat(h->lat_nb, h->d_jobs_fixed, B, h->P, th_dev, h->n_param, h->d_units, out_dev,
+                              h->d_lat_ctr, h->stream)) < 0)
+      return rc;
+    if (rc == 0) {
+      EWH_HIP(hipStreamSynchronize(h->stream));
+      std::memcpy(out_host, H->h_out, sizeof(double) * B);
+      H->last_split.assign(1, {0, (long long)H->P * B});
+      H->last_B = B;
+      h->last_B = B;
+      return 0;
+    }
+  }
   if ((rc = ensure_io(h, B))) return rc;
   DevCtx::Graph* hit = nullptr;
   for (auto& g : h->graphs)
@@ -2442,7 +2438,7 @@ int ewh_set_fixed_white(ewh_handle* H, const double* values) {
 
 int ewh_set_kernel_mode(ewh_handle* H, int32_t mode) {
   if (!H || mode < 0 || mode > 30) return set_err(EWH_E_INVALID, "bad handle / mode");
-  if (mode != 0 && mode != 1 && mode != 7 && !variant_built(mode))
+  if (mode != 0 && mode != 1 && mode != 2 && mode != 7 && !variant_built(mode))
     return set_err(EWH_E_UNSUPPORTED, "kernel mode " + std::to_string(mode) +
                                           " is not built into this library (A/B variants: the dev library, make dev)");
   for (DevCtx* h : H->ctx) {

@@ -15,14 +15,15 @@ constexpr int ITERS = 256;
 
 enum Op {
   NONE, MFMA, MFMA1, MFMA2, MFMA8, FMA_IND, FMA_DEP, FMACDPP_IND, FMACDPP_DEP, MOVDPP_IND, RLANE_IND, BPERM_IND, BPERM_DEP,
-  RCP_IND, RCP_DEP, CND_IND, NOP0, MUL_IND, FMAC_IND, NOP1, MFMA_ASM4, MFMA_ASM8
+  RCP_IND, RCP_DEP, CND_IND, NOP0, MUL_IND, FMAC_IND, NOP1, MFMA_ASM4, MFMA_ASM8, IADD_IND, SALU_IND, MOVB32_IND
 };
 static const char* NAMES[] = {"none", "mfma_f64_16x16x4 x4 chains", "mfma x1 chain", "mfma x2 chains", "mfma x8 chains", "v_fma_f64 indep", "v_fma_f64 dep chain",
                               "v_fmac_f64_dpp indep", "v_fmac_f64_dpp+s_nop1 dep", "v_mov_b64_dpp indep",
                               "v_readlane_b32 indep", "ds_bpermute_b32 indep", "ds_bpermute+wait dep",
                               "v_rcp_f64 indep", "v_rcp_f64 dep chain", "v_cndmask_b32 indep", "s_nop 0",
                               "v_mul_f64 indep", "v_fmac_f64_e32 indep", "s_nop 1",
-                              "asm mfma x4 acc (16/blk)", "asm mfma x8 acc (16/blk)"};
+                              "asm mfma x4 acc (16/blk)", "asm mfma x8 acc (16/blk)",
+                              "v_add_u32 indep", "s_add_u32 indep", "v_mov_b32 indep"};
 
 #define R16(x) x x x x x x x x x x x x x x x x
 
@@ -116,6 +117,26 @@ __device__ __forceinline__ void body(double* v, double w) {
                    : "+v"(acc[0]), "+v"(acc[1]), "+v"(acc[2]), "+v"(acc[3]), "+v"(acc[4]), "+v"(acc[5]), "+v"(acc[6]),
                      "+v"(acc[7]) : "v"(w), "v"(v[32]));
     }
+  } else if constexpr (OP == IADD_IND || OP == MOVB32_IND) {
+    int r[8];
+    for (int j = 0; j < 8; ++j) r[j] = (int)threadIdx.x + j;
+    if constexpr (OP == IADD_IND)
+      asm volatile(R16("v_add_u32 %0, %0, %8\n v_add_u32 %1, %1, %8\n v_add_u32 %2, %2, %8\n v_add_u32 %3, %3, %8\n"
+                       "v_add_u32 %4, %4, %8\n v_add_u32 %5, %5, %8\n v_add_u32 %6, %6, %8\n v_add_u32 %7, %7, %8\n")
+                   : "+v"(r[0]), "+v"(r[1]), "+v"(r[2]), "+v"(r[3]), "+v"(r[4]), "+v"(r[5]), "+v"(r[6]), "+v"(r[7])
+                   : "v"(__double2loint(w)));
+    else
+      asm volatile(R16("v_mov_b32 %0, %8\n v_mov_b32 %1, %8\n v_mov_b32 %2, %8\n v_mov_b32 %3, %8\n"
+                       "v_mov_b32 %4, %8\n v_mov_b32 %5, %8\n v_mov_b32 %6, %8\n v_mov_b32 %7, %8\n")
+                   : "+v"(r[0]), "+v"(r[1]), "+v"(r[2]), "+v"(r[3]), "+v"(r[4]), "+v"(r[5]), "+v"(r[6]), "+v"(r[7])
+                   : "v"(__double2loint(w)));
+    v[0] += r[0] + r[7];
+  } else if constexpr (OP == SALU_IND) {
+    int s0 = 1, s1 = 2, s2 = 3, s3 = 4;
+    asm volatile(R16("s_add_u32 %0, %0, 3\n s_add_u32 %1, %1, 5\n s_add_u32 %2, %2, 7\n s_add_u32 %3, %3, 9\n"
+                     "s_add_u32 %0, %0, 3\n s_add_u32 %1, %1, 5\n s_add_u32 %2, %2, 7\n s_add_u32 %3, %3, 9\n")
+                 : "+s"(s0), "+s"(s1), "+s"(s2), "+s"(s3) :: "scc");
+    v[0] += s0 + s1 + s2 + s3;
   } else if constexpr (OP == NOP1) {
     asm volatile(R16("s_nop 1\n s_nop 1\n s_nop 1\n s_nop 1\n s_nop 1\n s_nop 1\n s_nop 1\n s_nop 1\n") ::);
   }
@@ -183,6 +204,22 @@ int main() {
   run<MFMA_ASM8, FMACDPP_IND>(sink, cyc);
   run<MFMA_ASM8, BPERM_DEP>(sink, cyc);
   run<MFMA_ASM8, RCP_DEP>(sink, cyc);
+  // round 3: which non-fp64 classes co-issue beside a partner's f64 MFMA stream
+  run<NONE, CND_IND>(sink, cyc);
+  run<MFMA_ASM8, CND_IND>(sink, cyc);
+  run<NONE, RLANE_IND>(sink, cyc);
+  run<MFMA_ASM8, RLANE_IND>(sink, cyc);
+  run<NONE, IADD_IND>(sink, cyc);
+  run<MFMA_ASM8, IADD_IND>(sink, cyc);
+  run<NONE, MOVB32_IND>(sink, cyc);
+  run<MFMA_ASM8, MOVB32_IND>(sink, cyc);
+  run<NONE, SALU_IND>(sink, cyc);
+  run<MFMA_ASM8, SALU_IND>(sink, cyc);
+  run<NONE, BPERM_IND>(sink, cyc);
+  run<MFMA_ASM8, BPERM_IND>(sink, cyc);
+  run<MFMA_ASM8, MUL_IND>(sink, cyc);
+  run<MFMA_ASM8, RCP_IND>(sink, cyc);
+  run<MFMA_ASM8, MOVDPP_IND>(sink, cyc);
   run<MFMA1, NONE>(sink, cyc);
   run<MFMA2, NONE>(sink, cyc);
   run<MFMA, NONE>(sink, cyc);

@@ -178,3 +178,58 @@ def test_correlated_pulsar_partition(require_gpu):
     eng.corr_finish_device(th.data_ptr(), B, keep.data_ptr(), local.data_ptr(), out.data_ptr(), s)
     torch.cuda.synchronize()
     np.testing.assert_array_equal(out.cpu().numpy(), one)
+
+
+@pytest.mark.parametrize("name", ["c3_small", "c3_freesp", "c1_j1832", "c1_system", "full_c3"])
+def test_latency_kernel_matches_batched(require_gpu, c3, name):
+    """Batches of up to 16 samples on one device run chol_lat_kernel (one
+    4-wave workgroup per unit, theta read from pinned memory, the pulsar fold
+    and the lnL write fused into the launch).  Its factor, pivots and q are
+    the batched kernel's bit for bit; only the log-determinant sum is
+    associated differently, so lnL must agree with the batched path (kernel
+    mode 2: latency path off) far inside the strict bound, with the same -inf
+    pattern, for B = 1 (a sampler's single proposal), 5 and 16."""
+    from conftest import load_golden
+    if name == "full_c3":
+        pta = c3.pta
+        X = np.vstack([synth.prior_draws(pta, 8, 45), synth.near_draws(pta, c3.truth, 8, 3)])
+    else:
+        pta, X, _, _ = load_golden(name)
+    eng = pta.engine()
+    worst = 0.0
+    for B in (1, 5, 16):
+        XX = X[:B]
+        eng.set_kernel_mode(2)
+        ref = pta.get_lnlikelihood_batch(XX)
+        ref_terms = eng.unit_terms(B)
+        eng.set_kernel_mode(0)
+        got = pta.get_lnlikelihood_batch(XX)
+        terms = eng.unit_terms(B)
+        assert np.array_equal(np.isfinite(got), np.isfinite(ref)), f"{name} B={B}: -inf pattern differs"
+        assert not np.any(np.isnan(got))
+        fin = np.isfinite(ref)
+        err = np.abs(got[fin] - ref[fin]) / (1e-6 + 1e-10 * np.abs(ref[fin]))
+        worst = max(worst, float(err.max()) if err.size else 0.0)
+        assert np.all(err <= 1e-3), f"{name} B={B}: latency vs batched {err.max():.3e} of strict"
+        tf = np.isfinite(ref_terms)
+        assert np.array_equal(tf, np.isfinite(terms))
+        np.testing.assert_allclose(terms[tf], ref_terms[tf], rtol=1e-12, atol=1e-9)
+        # repeated single-proposal calls are deterministic
+        np.testing.assert_array_equal(pta.get_lnlikelihood_batch(XX), got)
+    print(f"{name}: latency vs batched max err/strict {worst:.3e}")
+
+
+def test_correlated_right_looking_small_chunks(require_gpu):
+    """Sigma_c of a correlated common process: chunks of up to 4 samples (a
+    PTMCMC proposal) are factored right-looking (trailing tiles updated in
+    parallel after each 64-wide panel), larger chunks left-looking (row
+    update, fused with the panel from 64 samples on).  Tile (i, j) takes the
+    same K = 64 slabs in the same order either way, so the two give the same
+    lnL bit for bit."""
+    from conftest import load_golden
+    pta, X, _, _ = load_golden("c5_small")
+    big = np.vstack([X] * 8)                    # 128 samples: left-looking, fused row update + panel
+    left = pta.get_lnlikelihood_batch(big)[:len(X)]
+    for B in (1, 3, 4):
+        got = np.concatenate([pta.get_lnlikelihood_batch(X[i:i + B]) for i in range(0, len(X), B)])
+        np.testing.assert_array_equal(got, left)
