@@ -34,6 +34,23 @@ namespace {
 
 constexpr int lat_owner(int i, int j) { return (i + j) & 3; }
 
+#ifdef EWH_DEV
+// phase stamps (dev mode 22): s_memtime per wave of the first LAT_STAMP_WG
+// workgroups -- 0 start, 1 theta staged, 2 phi^-1 ready, 3 + bb after the
+// barrier publishing panel bb's E (bb < NB - 1), 10 factorisation done,
+// 11 unit term combined, 12 end (after the fold, last workgroup only)
+constexpr int LAT_STAMP_WG = 64, LAT_STAMP_N = 16;
+__device__ long long g_lat_stamps[LAT_STAMP_WG * 4 * LAT_STAMP_N];
+#define LAT_STAMP(I)                                                                        \
+  if constexpr (STAMP) {                                                                    \
+    if (lane == 0 && blockIdx.x < LAT_STAMP_WG)                                             \
+      g_lat_stamps[(blockIdx.x * 4 + (threadIdx.x >> 6)) * LAT_STAMP_N + (I)] =             \
+          (long long)__builtin_amdgcn_s_memtime();                                           \
+  }
+#else
+#define LAT_STAMP(I)
+#endif
+
 template <int NB>
 struct LatLds {
   double phinv[16 * NB];
@@ -57,8 +74,8 @@ __device__ __forceinline__ v4d lds_get(const double (*src)[64], int lane) {
   return v;
 }
 
-template <int NB, int W>
-__device__ __forceinline__ void lat_wave(LatLds<NB>& S, const CholJob& J, const double* __restrict__ A,
+template <int NB, int W, bool STAMP>
+__device__ __forceinline__ void lat_wave(LatLds<NB>& S, const CholJob& J, const int* tidx, const double* __restrict__ A,
                                          const double* th, int ldth, int lane, LogAcc& ldet, bool& ok) {
   constexpr int LD = 16 * NB;
   const int tid = 64 * W + lane;
@@ -77,12 +94,21 @@ __device__ __forceinline__ void lat_wave(LatLds<NB>& S, const CholJob& J, const 
       }
     });
   });
+  LAT_STAMP(0)
   // ---- prologue: phi^-1 of every column (the arithmetic of chol_mfma_kernel) ----
-  const bool stage = ldth <= STAGE_THETA_MAX;
+  // theta -> LDS: the entries the staged records reference (their indices
+  // are positions in J.tidx), else the whole row when it fits
+  const bool compact = J.urec != nullptr && J.ntidx > 0;
+  const bool stage = compact || ldth <= STAGE_THETA_MAX;
   if (stage) {
-    for (int i = tid; i < ldth; i += 256) S.ths[i] = th[i];
+    if (compact) {
+      if (tid < J.ntidx) S.ths[tid] = th[tidx[tid]];   // (tidx: the job in global memory)
+    } else {
+      for (int i = tid; i < ldth; i += 256) S.ths[i] = th[i];
+    }
     __syncthreads();
   }
+  LAT_STAMP(1)
   const double* tp = stage ? S.ths : th;
   if (J.urec != nullptr) {
     for (int u = tid; u < J.nu; u += 256) {
@@ -129,6 +155,7 @@ __device__ __forceinline__ void lat_wave(LatLds<NB>& S, const CholJob& J, const 
     }
   }
   __syncthreads();
+  LAT_STAMP(2)
   static_for<0, NB>([&](auto I) {
     constexpr int i = decltype(I)::value;
     if constexpr (lat_owner(i, i) == W) {
@@ -158,6 +185,7 @@ __device__ __forceinline__ void lat_wave(LatLds<NB>& S, const CholJob& J, const 
   static_for<0, NB - 1>([&](auto BBc) {
     constexpr int bb = decltype(BBc)::value;
     __syncthreads();                                       // E, scales of panel bb
+    LAT_STAMP(3 + bb)
     constexpr bool row_owned = [] {
       for (int j = bb + 1; j < NB; ++j)
         if (lat_owner(bb, j) == W) return true;
@@ -211,9 +239,10 @@ __device__ __forceinline__ void lat_wave(LatLds<NB>& S, const CholJob& J, const 
       }
     });
   });
+  LAT_STAMP(10)
 }
 
-template <int NB>
+template <int NB, bool STAMP>
 __global__ __launch_bounds__(256) void chol_lat_kernel(const CholJob* __restrict__ jobs, int B, int P,
                                                        const double* theta, int ldth, double* __restrict__ out_units,
                                                        double* out, unsigned* counter) {
@@ -227,10 +256,10 @@ __global__ __launch_bounds__(256) void chol_lat_kernel(const CholJob* __restrict
   LogAcc ldet;
   bool ok = true;
   switch (w) {
-    case 0: lat_wave<NB, 0>(S, J, A, th, ldth, lane, ldet, ok); break;
-    case 1: lat_wave<NB, 1>(S, J, A, th, ldth, lane, ldet, ok); break;
-    case 2: lat_wave<NB, 2>(S, J, A, th, ldth, lane, ldet, ok); break;
-    default: lat_wave<NB, 3>(S, J, A, th, ldth, lane, ldet, ok); break;
+    case 0: lat_wave<NB, 0, STAMP>(S, J, jobs[p].tidx, A, th, ldth, lane, ldet, ok); break;
+    case 1: lat_wave<NB, 1, STAMP>(S, J, jobs[p].tidx, A, th, ldth, lane, ldet, ok); break;
+    case 2: lat_wave<NB, 2, STAMP>(S, J, jobs[p].tidx, A, th, ldth, lane, ldet, ok); break;
+    default: lat_wave<NB, 3, STAMP>(S, J, jobs[p].tidx, A, th, ldth, lane, ldet, ok); break;
   }
   const double lw = wave_sum(ldet.value());
   const bool okw = __all(ok);
@@ -239,6 +268,7 @@ __global__ __launch_bounds__(256) void chol_lat_kernel(const CholJob* __restrict
     S.ok[w] = okw ? 1 : 0;
   }
   __syncthreads();
+  LAT_STAMP(11)
   if (tid == 0) {
     double lnl = J.K[(long long)b * J.kstride] - 0.5 * S.qv - 0.5 * (((S.ldet[0] + S.ldet[1]) + S.ldet[2]) + S.ldet[3]);
     if (!(S.ok[0] && S.ok[1] && S.ok[2] && S.ok[3]) || J.fail) lnl = -INFINITY;
@@ -260,26 +290,44 @@ __global__ __launch_bounds__(256) void chol_lat_kernel(const CholJob* __restrict
     __threadfence_system();
     if (tid == 0) __hip_atomic_store(counter, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
   }
+  LAT_STAMP(12)
+}
+
+template <bool STAMP>
+int launch_chol_lat_t(int nb, const CholJob* jobs, int B, int P, const double* theta, int ldth, double* units,
+                      double* out, unsigned* counter, hipStream_t st) {
+  const dim3 grid((unsigned)(P * B)), block(256);
+#define EWH_LAT_CASE(N)                                                                                          \
+  case N:                                                                                                        \
+    hipLaunchKernelGGL(HIP_KERNEL_NAME(chol_lat_kernel<N, STAMP>), grid, block, 0, st, jobs, B, P, theta, ldth, \
+                       units, out, counter);                                                                     \
+    break;
+  switch (nb) {
+    EWH_LAT_CASE(1) EWH_LAT_CASE(2) EWH_LAT_CASE(3) EWH_LAT_CASE(4)
+    EWH_LAT_CASE(5) EWH_LAT_CASE(6) EWH_LAT_CASE(7) EWH_LAT_CASE(8)
+    default: return 1;
+  }
+#undef EWH_LAT_CASE
+  const hipError_t e = hipGetLastError();
+  return e == hipSuccess ? 0 : set_err(EWH_E_HIP, std::string("chol_lat_kernel: ") + hipGetErrorString(e));
 }
 
 }  // namespace
 
 int launch_chol_lat(int nb, const CholJob* jobs, int B, int P, const double* theta, int ldth, double* units,
-                    double* out, unsigned* counter, hipStream_t st) {
-  const dim3 grid((unsigned)(P * B)), block(256);
-  switch (nb) {
-    case 1: hipLaunchKernelGGL(chol_lat_kernel<1>, grid, block, 0, st, jobs, B, P, theta, ldth, units, out, counter); break;
-    case 2: hipLaunchKernelGGL(chol_lat_kernel<2>, grid, block, 0, st, jobs, B, P, theta, ldth, units, out, counter); break;
-    case 3: hipLaunchKernelGGL(chol_lat_kernel<3>, grid, block, 0, st, jobs, B, P, theta, ldth, units, out, counter); break;
-    case 4: hipLaunchKernelGGL(chol_lat_kernel<4>, grid, block, 0, st, jobs, B, P, theta, ldth, units, out, counter); break;
-    case 5: hipLaunchKernelGGL(chol_lat_kernel<5>, grid, block, 0, st, jobs, B, P, theta, ldth, units, out, counter); break;
-    case 6: hipLaunchKernelGGL(chol_lat_kernel<6>, grid, block, 0, st, jobs, B, P, theta, ldth, units, out, counter); break;
-    case 7: hipLaunchKernelGGL(chol_lat_kernel<7>, grid, block, 0, st, jobs, B, P, theta, ldth, units, out, counter); break;
-    case 8: hipLaunchKernelGGL(chol_lat_kernel<8>, grid, block, 0, st, jobs, B, P, theta, ldth, units, out, counter); break;
-    default: return 1;
-  }
-  const hipError_t e = hipGetLastError();
-  return e == hipSuccess ? 0 : set_err(EWH_E_HIP, std::string("chol_lat_kernel: ") + hipGetErrorString(e));
+                    double* out, unsigned* counter, hipStream_t st, bool stamp) {
+#ifdef EWH_DEV
+  if (stamp) return launch_chol_lat_t<true>(nb, jobs, B, P, theta, ldth, units, out, counter, st);
+#endif
+  (void)stamp;
+  return launch_chol_lat_t<false>(nb, jobs, B, P, theta, ldth, units, out, counter, st);
 }
+
+#ifdef EWH_DEV
+extern "C" int ewh_dev_lat_stamps(long long* out, long long n) {
+  if (n > (long long)LAT_STAMP_WG * 4 * LAT_STAMP_N) n = (long long)LAT_STAMP_WG * 4 * LAT_STAMP_N;
+  return hipMemcpyFromSymbol(out, HIP_SYMBOL(g_lat_stamps), (size_t)n * sizeof(long long)) == hipSuccess ? 0 : -1;
+}
+#endif
 
 }  // namespace ewh_dev

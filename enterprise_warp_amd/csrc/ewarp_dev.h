@@ -237,6 +237,10 @@ struct CholJob {
   // NULL: the CSR path (a spectrum with more than URec::NE entries)
   const struct URec* urec = nullptr;
   const int* urep = nullptr;
+  // the theta entries the records reference, staged alone (their DSpec
+  // indices are positions in this list); 0: the whole theta row is staged
+  int ntidx = 0;
+  int tidx[16] = {};
 };
 
 // one distinct spectrum of a fixed-WN job: phi = sum of its ne entries
@@ -246,6 +250,7 @@ struct URec {
   int ne, pad_[3];
 };
 constexpr int STAGE_THETA_MAX = 512;   // theta row staged in LDS up to this many parameters
+constexpr int TIDX_MAX = 16;           // CholJob::tidx
 
 // ----------------------------------------------------------------------------
 // fp64 MFMA contraction G = T_aug^T W T_aug - sum_e beta_e s_e s_e^T
@@ -943,16 +948,21 @@ void chol_mfma_kernel(const CholJob* __restrict__ jobs, int B, long long u0, int
   // log|phi| is summed into the per-lane log-det accumulator (one log() at
   // the end of the kernel)
   LogAcc ldet;
-  if (J.urec != nullptr && ldth <= STAGE_THETA_MAX) {
-    // staged: theta row -> LDS, each distinct spectrum's record by its lane,
-    // every column's record index -- all loads issued together
+  if (J.urec != nullptr && (J.ntidx > 0 || ldth <= STAGE_THETA_MAX)) {
+    // staged: the theta entries the spectra read (or the whole row) -> LDS,
+    // each distinct spectrum's record by its lane, every column's record
+    // index -- all loads issued together
     __shared__ double ths[STAGE_THETA_MAX];
     int ur[(LD + 63) / 64];
     static_for<0, (LD + 63) / 64>([&](auto I) {
       constexpr int i = decltype(I)::value;
       ur[i] = 64 * i + lane < J.mreal ? J.urep[64 * i + lane] : -1;
     });
-    for (int i = lane; i < ldth; i += 64) ths[i] = th[i];
+    if (J.ntidx > 0) {
+      if (lane < J.ntidx) ths[lane] = th[jobs[p].tidx[lane]];
+    } else {
+      for (int i = lane; i < ldth; i += 64) ths[i] = th[i];
+    }
     __syncthreads();
     for (int u = lane; u < J.nu; u += 64) {
       const URec& R = J.urec[u];
@@ -1271,7 +1281,7 @@ int launch_chol_big_nb(int nb, const CholJob* jobs, int B, long long u0, long lo
 // Returns 1 if nb has no latency kernel (caller uses the batched path).
 constexpr int LAT_NB_MAX = 8;
 int launch_chol_lat(int nb, const CholJob* jobs, int B, int P, const double* theta, int ldth, double* units,
-                    double* out, unsigned* counter, hipStream_t st);
+                    double* out, unsigned* counter, hipStream_t st, bool stamp = false);
 // keep_out: pulsar-major kept blocks, keep_bs samples per pulsar (see chol_mfma_kernel KEEP)
 int launch_partial_nb(int nb, int keep, const CholJob* jobs, int B, long long u0, long long n,
                       const double* theta, int ldth, double* units, double* keep_out, int keep_bs, hipStream_t st);

@@ -1133,6 +1133,7 @@ struct PsrHost {
   int* d_fx_ulist = nullptr;      // the distinct-spectrum columns
   int fx_nu = 0;
   URec* d_fx_urec = nullptr;      // the distinct spectra with their entries inline (NULL: > URec::NE entries)
+  std::vector<int> fx_tidx;       // theta entries the records read (their indices point here); empty: the whole row
   int* d_fx_urep = nullptr;       // fixed columns -> distinct-spectrum record (-1: no entry)
   double* d_S = nullptr;          // fx_ld^2
   bool has_theta_white = false;
@@ -1504,6 +1505,10 @@ int setup_fixed(DevCtx* h) {
     const int mreal = h->osmode ? ps.fx_ld - 1 : ps.nloc;
     jobs[p] = CholJob{ps.d_S, 0, ps.fx_ld, mreal, ps.d_fx_colptr, ps.d_fx_spec, h->d_fxK + p, 0, 0,
                       ps.d_fx_rep, ps.d_fx_ulist, ps.fx_nu, h->stage_spectra ? ps.d_fx_urec : nullptr, ps.d_fx_urep};
+    if (jobs[p].urec != nullptr) {
+      jobs[p].ntidx = (int)ps.fx_tidx.size();
+      for (int i = 0; i < jobs[p].ntidx; ++i) jobs[p].tidx[i] = ps.fx_tidx[i];
+    }
   }
   EWH_HIP(hipMemcpyAsync(fails.data(), h->d_fxfail, sizeof(int) * h->P, hipMemcpyDeviceToHost, h->stream));
   EWH_HIP(hipStreamSynchronize(h->stream));
@@ -1955,6 +1960,25 @@ int create_ctx(const ewh_pta_desc* d, const std::vector<ProjCoef>& proj, int dev
         urec[u].ne = std::min(ne, URec::NE);
         for (int e = 0; e < urec[u].ne; ++e) urec[u].e[e] = ent[ptr[a] + e];
       }
+      // the theta entries the records read: staged alone when there are at
+      // most TIDX_MAX of them (the records then index that list)
+      std::vector<int> tl;
+      for (size_t u = 0; u < ulist.size(); ++u)
+        for (int e = 0; e < urec[u].ne; ++e)
+          for (int idx : {urec[u].e[e].i0, urec[u].e[e].i1, urec[u].e[e].i2})
+            if (idx >= 0 && std::find(tl.begin(), tl.end(), idx) == tl.end()) tl.push_back(idx);
+      std::sort(tl.begin(), tl.end());
+      ps.fx_tidx.clear();
+      if (fits && (int)tl.size() <= TIDX_MAX) {
+        ps.fx_tidx = tl;
+        auto pos = [&](int idx) { return idx < 0 ? idx : (int)(std::lower_bound(tl.begin(), tl.end(), idx) - tl.begin()); };
+        for (size_t u = 0; u < ulist.size(); ++u)
+          for (int e = 0; e < urec[u].ne; ++e) {
+            urec[u].e[e].i0 = pos(urec[u].e[e].i0);
+            urec[u].e[e].i1 = pos(urec[u].e[e].i1);
+            urec[u].e[e].i2 = pos(urec[u].e[e].i2);
+          }
+      }
       for (size_t a = 0; a < rep.size(); ++a)
         if (ptr[a] < ptr[a + 1]) urep[a] = uidx[rep[a]];
       if (fits) {
@@ -2208,6 +2232,9 @@ struct ewh_handle {
   double* d_part = nullptr;
   size_t part_cap = 0;
   std::vector<hipEvent_t> ev;
+  // latency path: device addresses of h_theta / h_out (for the host pointers recorded)
+  const double *lat_th_host = nullptr, *lat_out_host = nullptr;
+  double *lat_th_dev = nullptr, *lat_out_dev = nullptr;
 };
 
 namespace {
@@ -2312,15 +2339,22 @@ int lnl_batch_single(ewh_handle* H, DevCtx* h, int B, double* out_host) {
   int rc;
   EWH_HIP(hipSetDevice(h->device));
   if ((rc = ensure_pinned(&H->h_out, &H->h_out_cap, (size_t)B))) return rc;
-  if (h->lat_nb > 0 && B <= LAT_B_MAX && h->kernel_mode == 0) {
+  if (h->lat_nb > 0 && B <= LAT_B_MAX && (h->kernel_mode == 0 || h->kernel_mode == 22)) {
     // latency path: one launch reads theta from the pinned staging, folds
     // the unit terms and writes lnL to pinned memory (chol_lat.hip)
     if ((rc = ensure_units(h, B))) return rc;
-    double *th_dev = nullptr, *out_dev = nullptr;
-    EWH_HIP(hipHostGetDevicePointer((void**)&th_dev, H->h_theta, 0));
-    EWH_HIP(hipHostGetDevicePointer((void**)&out_dev, H->h_out, 0));
+    // device addresses of the pinned staging (looked up again only after a reallocation)
+    if (H->lat_th_host != H->h_theta) {
+      EWH_HIP(hipHostGetDevicePointer((void**)&H->lat_th_dev, H->h_theta, 0));
+      H->lat_th_host = H->h_theta;
+    }
+    if (H->lat_out_host != H->h_out) {
+      EWH_HIP(hipHostGetDevicePointer((void**)&H->lat_out_dev, H->h_out, 0));
+      H->lat_out_host = H->h_out;
+    }
+    double *th_dev = H->lat_th_dev, *out_dev = H->lat_out_dev;
     if ((rc = launch_chol_lat(h->lat_nb, h->d_jobs_fixed, B, h->P, th_dev, h->n_param, h->d_units, out_dev,
-                              h->d_lat_ctr, h->stream)) < 0)
+                              h->d_lat_ctr, h->stream, h->kernel_mode == 22)) < 0)
       return rc;
     if (rc == 0) {
       EWH_HIP(hipStreamSynchronize(h->stream));

@@ -5,7 +5,8 @@ the dominant kernel (CPU only; reads gpurun_out/pmc_<tag>_*).
 
 Writes profiles/<tag>/pmc_summary.json (every kernel, every counter: mean per
 dispatch, dispatch count) and profiles/pmc_chol.json, which bench.py reads for
-`roofline.traffic`.  HBM bytes per launch follow MI355X_MICROARCH.md § HBM:
+`roofline.traffic` (with the kernel-source sha the profiling run recorded in
+gpurun_out/pmc_<tag>_sha.txt).  HBM bytes per launch follow MI355X_MICROARCH.md § HBM:
 FETCH_SIZE and WRITE_SIZE are in KiB, and on gfx950 FETCH_SIZE reports half
 the bytes of wide coalesced reads, so bytes = (2 * FETCH_SIZE + WRITE_SIZE)
 * 1024.  The SQ counters are per dispatch totals over all waves.
@@ -71,9 +72,14 @@ def main():
     if "SQ_WAVES" in sq:
         waves = sq["SQ_WAVES"]["mean"]
         rec["per_wave"] = {n: sq[n]["mean"] / waves for n in sq if n.startswith("SQ_") and n != "SQ_WAVES"}
-    sys.path.insert(0, ROOT)
-    from bench import kernel_sources_sha
-    rec["kernel_sources_sha"] = kernel_sources_sha()
+    # the sha of the PROFILED kernel sources, recorded on the GPU box by the
+    # profiling script (gpurun_out/pmc_<tag>_sha.txt); bench.py uses the
+    # traffic only while its own tree has the same sha
+    shaf = os.path.join(args.src, f"pmc_{args.tag}_sha.txt")
+    if not os.path.exists(shaf):
+        raise SystemExit(f"{shaf} missing: the profiling run must record bench.kernel_sources_sha()")
+    with open(shaf) as fh:
+        rec["kernel_sources_sha"] = fh.read().split()[-1]
     with open(os.path.join(ROOT, "profiles", "pmc_chol.json"), "w") as fh:
         json.dump(rec, fh, indent=1)
     print(json.dumps(rec, indent=1))

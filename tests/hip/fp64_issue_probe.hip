@@ -15,7 +15,7 @@ constexpr int ITERS = 256;
 
 enum Op {
   NONE, MFMA, MFMA1, MFMA2, MFMA8, FMA_IND, FMA_DEP, FMACDPP_IND, FMACDPP_DEP, MOVDPP_IND, RLANE_IND, BPERM_IND, BPERM_DEP,
-  RCP_IND, RCP_DEP, CND_IND, NOP0, MUL_IND, FMAC_IND, NOP1, MFMA_ASM4, MFMA_ASM8, IADD_IND, SALU_IND, MOVB32_IND
+  RCP_IND, RCP_DEP, CND_IND, NOP0, MUL_IND, FMAC_IND, NOP1, MFMA_ASM4, MFMA_ASM8, IADD_IND, SALU_IND, MOVB32_IND, MFMA_PAD, MFMA_PAD_FMA
 };
 static const char* NAMES[] = {"none", "mfma_f64_16x16x4 x4 chains", "mfma x1 chain", "mfma x2 chains", "mfma x8 chains", "v_fma_f64 indep", "v_fma_f64 dep chain",
                               "v_fmac_f64_dpp indep", "v_fmac_f64_dpp+s_nop1 dep", "v_mov_b64_dpp indep",
@@ -23,7 +23,8 @@ static const char* NAMES[] = {"none", "mfma_f64_16x16x4 x4 chains", "mfma x1 cha
                               "v_rcp_f64 indep", "v_rcp_f64 dep chain", "v_cndmask_b32 indep", "s_nop 0",
                               "v_mul_f64 indep", "v_fmac_f64_e32 indep", "s_nop 1",
                               "asm mfma x4 acc (16/blk)", "asm mfma x8 acc (16/blk)",
-                              "v_add_u32 indep", "s_add_u32 indep", "v_mov_b32 indep"};
+                              "v_add_u32 indep", "s_add_u32 indep", "v_mov_b32 indep",
+                              "mfma + s_nop 7,6 (60 cyc)", "8 mfma + 8 own fma (per mfma)"};
 
 #define R16(x) x x x x x x x x x x x x x x x x
 
@@ -137,6 +138,43 @@ __device__ __forceinline__ void body(double* v, double w) {
                      "s_add_u32 %0, %0, 3\n s_add_u32 %1, %1, 5\n s_add_u32 %2, %2, 7\n s_add_u32 %3, %3, 9\n")
                  : "+s"(s0), "+s"(s1), "+s"(s2), "+s"(s3) :: "scc");
     v[0] += s0 + s1 + s2 + s3;
+  } else if constexpr (OP == MFMA_PAD || OP == MFMA_PAD_FMA) {
+    // 16 MFMAs round-robin over 8 accumulators; after each, either ~60 cycles
+    // of s_nop (the wave presents no instruction while the pipe is busy) or
+    // 8 independent v_fma_f64 of its own
+    typedef double v4d __attribute__((ext_vector_type(4)));
+    v4d* acc = reinterpret_cast<v4d*>(v);
+    if constexpr (OP == MFMA_PAD) {
+      asm volatile(R16("v_mfma_f64_16x16x4_f64 %0, %8, %9, %0\n s_nop 7\n s_nop 6\n"
+                       "v_mfma_f64_16x16x4_f64 %1, %8, %9, %1\n s_nop 7\n s_nop 6\n"
+                       "v_mfma_f64_16x16x4_f64 %2, %8, %9, %2\n s_nop 7\n s_nop 6\n"
+                       "v_mfma_f64_16x16x4_f64 %3, %8, %9, %3\n s_nop 7\n s_nop 6\n"
+                       "v_mfma_f64_16x16x4_f64 %4, %8, %9, %4\n s_nop 7\n s_nop 6\n"
+                       "v_mfma_f64_16x16x4_f64 %5, %8, %9, %5\n s_nop 7\n s_nop 6\n"
+                       "v_mfma_f64_16x16x4_f64 %6, %8, %9, %6\n s_nop 7\n s_nop 6\n"
+                       "v_mfma_f64_16x16x4_f64 %7, %8, %9, %7\n s_nop 7\n s_nop 6\n")
+                   : "+v"(acc[0]), "+v"(acc[1]), "+v"(acc[2]), "+v"(acc[3]), "+v"(acc[4]), "+v"(acc[5]), "+v"(acc[6]),
+                     "+v"(acc[7]) : "v"(w), "v"(v[32]));
+    } else {
+      double f0 = v[33], f1 = v[34], f2 = v[35], f3 = v[36];
+      asm volatile(R16("v_mfma_f64_16x16x4_f64 %[a0], %[w], %[x], %[a0]\n"
+                       "v_fma_f64 %[f0], %[w], %[w], %[f0]\n v_fma_f64 %[f1], %[w], %[w], %[f1]\n"
+                       "v_fma_f64 %[f2], %[w], %[w], %[f2]\n v_fma_f64 %[f3], %[w], %[w], %[f3]\n"
+                       "v_fma_f64 %[f0], %[w], %[w], %[f0]\n v_fma_f64 %[f1], %[w], %[w], %[f1]\n"
+                       "v_fma_f64 %[f2], %[w], %[w], %[f2]\n v_fma_f64 %[f3], %[w], %[w], %[f3]\n"
+                       "v_mfma_f64_16x16x4_f64 %[a1], %[w], %[x], %[a1]\n"
+                       "v_mfma_f64_16x16x4_f64 %[a2], %[w], %[x], %[a2]\n"
+                       "v_mfma_f64_16x16x4_f64 %[a3], %[w], %[x], %[a3]\n"
+                       "v_mfma_f64_16x16x4_f64 %[a4], %[w], %[x], %[a4]\n"
+                       "v_mfma_f64_16x16x4_f64 %[a5], %[w], %[x], %[a5]\n"
+                       "v_mfma_f64_16x16x4_f64 %[a6], %[w], %[x], %[a6]\n"
+                       "v_mfma_f64_16x16x4_f64 %[a7], %[w], %[x], %[a7]\n")
+                   : [a0] "+v"(acc[0]), [a1] "+v"(acc[1]), [a2] "+v"(acc[2]), [a3] "+v"(acc[3]), [a4] "+v"(acc[4]),
+                     [a5] "+v"(acc[5]), [a6] "+v"(acc[6]), [a7] "+v"(acc[7]), [f0] "+v"(f0), [f1] "+v"(f1),
+                     [f2] "+v"(f2), [f3] "+v"(f3)
+                   : [w] "v"(w), [x] "v"(v[32]));
+      v[33] = f0 + f1 + f2 + f3;
+    }
   } else if constexpr (OP == NOP1) {
     asm volatile(R16("s_nop 1\n s_nop 1\n s_nop 1\n s_nop 1\n s_nop 1\n s_nop 1\n s_nop 1\n s_nop 1\n") ::);
   }
@@ -144,7 +182,7 @@ __device__ __forceinline__ void body(double* v, double w) {
 
 // instructions per body() call
 constexpr int per_call(int op) {
-  return op == MFMA_ASM4 ? 64 : op == MFMA_ASM8 ? 128 : op == MFMA || op == MFMA1 || op == MFMA2 || op == MFMA8 ? 16 : op == FMA_DEP || op == FMACDPP_DEP || op == RCP_DEP || op == BPERM_DEP ? 16
+  return op == MFMA_ASM4 ? 64 : op == MFMA_ASM8 ? 128 : op == MFMA_PAD ? 128 : op == MFMA_PAD_FMA ? 128 : op == MFMA || op == MFMA1 || op == MFMA2 || op == MFMA8 ? 16 : op == FMA_DEP || op == FMACDPP_DEP || op == RCP_DEP || op == BPERM_DEP ? 16
        : op == RLANE_IND || op == CND_IND ? 64 : 128;
 }
 
@@ -220,6 +258,16 @@ int main() {
   run<MFMA_ASM8, MUL_IND>(sink, cyc);
   run<MFMA_ASM8, RCP_IND>(sink, cyc);
   run<MFMA_ASM8, MOVDPP_IND>(sink, cyc);
+  // round 3: an MFMA stream that presents no instruction while the pipe is
+  // busy (s_nop padding): does the partner then issue, and does its f64 VALU
+  // run beside the matrix core?
+  run<MFMA_PAD, NONE>(sink, cyc);
+  run<MFMA_PAD, FMA_IND>(sink, cyc);
+  run<MFMA_PAD, IADD_IND>(sink, cyc);
+  run<MFMA_PAD, CND_IND>(sink, cyc);
+  run<MFMA_PAD, RLANE_IND>(sink, cyc);
+  run<MFMA_PAD, FMACDPP_IND>(sink, cyc);
+  run<MFMA_PAD_FMA, NONE>(sink, cyc);
   run<MFMA1, NONE>(sink, cyc);
   run<MFMA2, NONE>(sink, cyc);
   run<MFMA, NONE>(sink, cyc);
