@@ -80,7 +80,16 @@ __device__ __forceinline__ void lat_wave(LatLds<NB>& S, const CholJob& J, const 
   constexpr int LD = 16 * NB;
   const int tid = 64 * W + lane;
   const int q = lane >> 4, c = lane & 15;
-  // owned blocks, loaded before the prologue (their latency overlaps it)
+  LAT_STAMP(0)
+  // ---- prologue: phi^-1 of every column (the arithmetic of chol_mfma_kernel) ----
+  // theta -> LDS: the entries the staged records reference (their indices
+  // are positions in J.tidx), else the whole row when it fits.  theta sits in
+  // pinned host memory: its load is issued first, ahead of the block loads
+  const bool compact = J.urec != nullptr && J.ntidx > 0;
+  const bool stage = compact || ldth <= STAGE_THETA_MAX;
+  double tv = 0.0;
+  if (compact && tid < J.ntidx) tv = th[tidx[tid]];   // (tidx: the job in global memory)
+  // owned blocks (their latency overlaps the prologue)
   v4d C[NB][NB];
   static_for<0, NB>([&](auto I) {
     constexpr int i = decltype(I)::value;
@@ -94,15 +103,9 @@ __device__ __forceinline__ void lat_wave(LatLds<NB>& S, const CholJob& J, const 
       }
     });
   });
-  LAT_STAMP(0)
-  // ---- prologue: phi^-1 of every column (the arithmetic of chol_mfma_kernel) ----
-  // theta -> LDS: the entries the staged records reference (their indices
-  // are positions in J.tidx), else the whole row when it fits
-  const bool compact = J.urec != nullptr && J.ntidx > 0;
-  const bool stage = compact || ldth <= STAGE_THETA_MAX;
   if (stage) {
     if (compact) {
-      if (tid < J.ntidx) S.ths[tid] = th[tidx[tid]];   // (tidx: the job in global memory)
+      if (tid < J.ntidx) S.ths[tid] = tv;
     } else {
       for (int i = tid; i < ldth; i += 256) S.ths[i] = th[i];
     }
@@ -279,12 +282,23 @@ __global__ __launch_bounds__(256) void chol_lat_kernel(const CholJob* __restrict
   }
   __syncthreads();
   if (S.last) {
-    // the last unit to finish: lnL_b = sum over pulsars in pulsar order
+    // the last unit to finish: lnL_b = sum over pulsars in pulsar order.  The
+    // P B terms are loaded in parallel into LDS (one load latency, not P),
+    // then each sample's thread adds its column in pulsar order
     __threadfence();
+    double* stage_units = &S.U[0][0][0];                  // (free now: >= 256 NB doubles)
+    constexpr int CAP = NB * 256;
+    const bool staged = P * B <= CAP;
+    if (staged) {
+      for (int i = tid; i < P * B; i += 256)
+        stage_units[i] = __hip_atomic_load(out_units + i, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      __syncthreads();
+    }
     for (int bq = tid; bq < B; bq += 256) {
       double s = 0.0;
       for (int pp = 0; pp < P; ++pp)
-        s += __hip_atomic_load(out_units + (long long)pp * B + bq, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        s += staged ? stage_units[pp * B + bq]
+                    : __hip_atomic_load(out_units + (long long)pp * B + bq, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
       out[bq] = s;
     }
     __threadfence_system();

@@ -2333,7 +2333,7 @@ int lnl_batch_corr_pulsars(ewh_handle* H, int B, double* out_host) {
 // One device: replay the captured graph of this batch size when there is one;
 // otherwise run the batch eagerly (that also sizes every scratch buffer) and
 // capture the same sequence for the next call.
-constexpr int LAT_B_MAX = 16;   // batches up to this size take the latency kernel
+constexpr int LAT_B_MAX = 8;    // batches up to this size take the latency kernel (profiles/r03c/latency.log: B = 16 is faster batched)
 
 int lnl_batch_single(ewh_handle* H, DevCtx* h, int B, double* out_host) {
   int rc;

@@ -254,7 +254,7 @@ double ewh_unit_cost(const ewh_handle* h, int32_t pulsar);
  * two-level LDL^T panel -- the 16x16 diagonal block in 4-row sub-panels by
  * VALU, each closed by one symmetric MFMA rank-4 update, the rest of the
  * block row by MFMA with L^-1 -- when the matrix fits registers; the LDS
- * kernel otherwise; batches of up to 16 samples on one device take the
+ * kernel otherwise; batches of up to 8 samples on one device take the
  * latency kernel, one 4-wave workgroup per (pulsar, sample) with theta read
  * from pinned memory and the pulsar fold fused), 2 = the default without
  * that latency path (batched kernels at every batch size), 1 = force the
