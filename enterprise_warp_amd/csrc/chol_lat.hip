@@ -23,10 +23,11 @@
 // four waves): strict-equal to the batched kernel, not bit-identical.
 //
 // Sampler I/O is fused in: theta is read straight from the handle's pinned
-// (host-mapped) staging, the last workgroup to finish folds the unit terms
-// over pulsars in pulsar order (the left fold of reduce_units_kernel: the
-// same value the batched path returns) and writes lnL to pinned host memory.
-// One launch per call: no H2D / memset / reduction / D2H operations.
+// (host-mapped) staging and every unit writes its term to pinned host memory
+// as well; the host folds the P terms of a sample in pulsar order (the left
+// fold of reduce_units_kernel).  One launch per call: no H2D / memset /
+// reduction / D2H operations, and no cross-workgroup atomics (a fold by the
+// last workgroup cost ~4k cycles of agent-scope fences and atomics).
 #include "ewarp_dev.h"
 
 namespace ewh_dev {
@@ -38,7 +39,7 @@ constexpr int lat_owner(int i, int j) { return (i + j) & 3; }
 // phase stamps (dev mode 22): s_memtime per wave of the first LAT_STAMP_WG
 // workgroups -- 0 start, 1 theta staged, 2 phi^-1 ready, 3 + bb after the
 // barrier publishing panel bb's E (bb < NB - 1), 10 factorisation done,
-// 11 unit term combined, 12 end (after the fold, last workgroup only)
+// 11 unit term combined
 constexpr int LAT_STAMP_WG = 64, LAT_STAMP_N = 16;
 __device__ long long g_lat_stamps[LAT_STAMP_WG * 4 * LAT_STAMP_N];
 #define LAT_STAMP(I)                                                                        \
@@ -62,7 +63,6 @@ struct LatLds {
   double ldet[4];
   int ok[4];
   double qv;
-  int last;
 };
 
 __device__ __forceinline__ void lds_put(double (*dst)[64], const v4d& v, int lane) {
@@ -83,13 +83,11 @@ __device__ __forceinline__ void lat_wave(LatLds<NB>& S, const CholJob& J, const 
   LAT_STAMP(0)
   // ---- prologue: phi^-1 of every column (the arithmetic of chol_mfma_kernel) ----
   // theta -> LDS: the entries the staged records reference (their indices
-  // are positions in J.tidx), else the whole row when it fits.  theta sits in
-  // pinned host memory: its load is issued first, ahead of the block loads
+  // are positions in J.tidx), else the whole row when it fits
   const bool compact = J.urec != nullptr && J.ntidx > 0;
   const bool stage = compact || ldth <= STAGE_THETA_MAX;
-  double tv = 0.0;
-  if (compact && tid < J.ntidx) tv = th[tidx[tid]];   // (tidx: the job in global memory)
-  // owned blocks (their latency overlaps the prologue)
+  // owned blocks (their latency overlaps the prologue; issuing the theta load
+  // ahead of them measured slower: its wait then covered every block load)
   v4d C[NB][NB];
   static_for<0, NB>([&](auto I) {
     constexpr int i = decltype(I)::value;
@@ -105,7 +103,7 @@ __device__ __forceinline__ void lat_wave(LatLds<NB>& S, const CholJob& J, const 
   });
   if (stage) {
     if (compact) {
-      if (tid < J.ntidx) S.ths[tid] = tv;
+      if (tid < J.ntidx) S.ths[tid] = th[tidx[tid]];   // (tidx: the job in global memory)
     } else {
       for (int i = tid; i < ldth; i += 256) S.ths[i] = th[i];
     }
@@ -175,7 +173,7 @@ __device__ __forceinline__ void lat_wave(LatLds<NB>& S, const CholJob& J, const 
   // factor diagonal block BB (owner only); publish E and the scales, or q
   auto factor = [&](auto BBc) {
     constexpr int bb = decltype(BBc)::value;
-    diag_factor_2l<NB, bb, true>(C[bb][bb], E, rsr, q, c, ldet, ok, klast);
+    diag_factor_2l<NB, bb, true, true>(C[bb][bb], E, rsr, q, c, ldet, ok, klast);
     if constexpr (bb < NB - 1) {
       lds_put(S.E, E, lane);
       static_for<0, 4>([&](auto R) { S.R[decltype(R)::value][lane] = rsr[decltype(R)::value]; });
@@ -248,9 +246,10 @@ __device__ __forceinline__ void lat_wave(LatLds<NB>& S, const CholJob& J, const 
 template <int NB, bool STAMP>
 __global__ __launch_bounds__(256) void chol_lat_kernel(const CholJob* __restrict__ jobs, int B, int P,
                                                        const double* theta, int ldth, double* __restrict__ out_units,
-                                                       double* out, unsigned* counter) {
+                                                       double* host_units) {
   __shared__ LatLds<NB> S;
   const int tid = threadIdx.x, w = tid >> 6, lane = tid & 63;
+  (void)P;
   const int u = blockIdx.x;
   const int p = u / B, b = u % B;
   const CholJob J = jobs[p];
@@ -275,46 +274,20 @@ __global__ __launch_bounds__(256) void chol_lat_kernel(const CholJob* __restrict
   if (tid == 0) {
     double lnl = J.K[(long long)b * J.kstride] - 0.5 * S.qv - 0.5 * (((S.ldet[0] + S.ldet[1]) + S.ldet[2]) + S.ldet[3]);
     if (!(S.ok[0] && S.ok[1] && S.ok[2] && S.ok[3]) || J.fail) lnl = -INFINITY;
-    __hip_atomic_store(out_units + (long long)p * B + b, lnl, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    __threadfence();
-    const unsigned t = __hip_atomic_fetch_add(counter, 1u, __ATOMIC_ACQ_REL, __HIP_MEMORY_SCOPE_AGENT);
-    S.last = t == gridDim.x - 1;
-  }
-  __syncthreads();
-  if (S.last) {
-    // the last unit to finish: lnL_b = sum over pulsars in pulsar order.  The
-    // P B terms are loaded in parallel into LDS (one load latency, not P),
-    // then each sample's thread adds its column in pulsar order
-    __threadfence();
-    double* stage_units = &S.U[0][0][0];                  // (free now: >= 256 NB doubles)
-    constexpr int CAP = NB * 256;
-    const bool staged = P * B <= CAP;
-    if (staged) {
-      for (int i = tid; i < P * B; i += 256)
-        stage_units[i] = __hip_atomic_load(out_units + i, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-      __syncthreads();
-    }
-    for (int bq = tid; bq < B; bq += 256) {
-      double s = 0.0;
-      for (int pp = 0; pp < P; ++pp)
-        s += staged ? stage_units[pp * B + bq]
-                    : __hip_atomic_load(out_units + (long long)pp * B + bq, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-      out[bq] = s;
-    }
-    __threadfence_system();
-    if (tid == 0) __hip_atomic_store(counter, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    out_units[(long long)p * B + b] = lnl;
+    host_units[(long long)p * B + b] = lnl;    // pinned: the host folds the P terms after the launch
   }
   LAT_STAMP(12)
 }
 
 template <bool STAMP>
 int launch_chol_lat_t(int nb, const CholJob* jobs, int B, int P, const double* theta, int ldth, double* units,
-                      double* out, unsigned* counter, hipStream_t st) {
+                      double* host_units, hipStream_t st) {
   const dim3 grid((unsigned)(P * B)), block(256);
 #define EWH_LAT_CASE(N)                                                                                          \
   case N:                                                                                                        \
     hipLaunchKernelGGL(HIP_KERNEL_NAME(chol_lat_kernel<N, STAMP>), grid, block, 0, st, jobs, B, P, theta, ldth, \
-                       units, out, counter);                                                                     \
+                       units, host_units);                                                                       \
     break;
   switch (nb) {
     EWH_LAT_CASE(1) EWH_LAT_CASE(2) EWH_LAT_CASE(3) EWH_LAT_CASE(4)
@@ -329,12 +302,12 @@ int launch_chol_lat_t(int nb, const CholJob* jobs, int B, int P, const double* t
 }  // namespace
 
 int launch_chol_lat(int nb, const CholJob* jobs, int B, int P, const double* theta, int ldth, double* units,
-                    double* out, unsigned* counter, hipStream_t st, bool stamp) {
+                    double* host_units, hipStream_t st, bool stamp) {
 #ifdef EWH_DEV
-  if (stamp) return launch_chol_lat_t<true>(nb, jobs, B, P, theta, ldth, units, out, counter, st);
+  if (stamp) return launch_chol_lat_t<true>(nb, jobs, B, P, theta, ldth, units, host_units, st);
 #endif
   (void)stamp;
-  return launch_chol_lat_t<false>(nb, jobs, B, P, theta, ldth, units, out, counter, st);
+  return launch_chol_lat_t<false>(nb, jobs, B, P, theta, ldth, units, host_units, st);
 }
 
 #ifdef EWH_DEV

@@ -701,7 +701,28 @@ struct NoHook {
 // c == 0 of each row) and d_k > 0.  RL: the last column of block row NB-1 is
 // the residual (not pivoted); klim: pivots >= klim of that block row are pads
 // (identity rows and columns: pivot 1, every multiplier 0) and are skipped.
-template <int NB, int BB, bool RL>
+// Rr[j] += Rr[j] (lane k of its row) * nw for the rows j in (KQ, 4): the
+// replicated copies of the sub-panel's rows, updated exactly as pivot_fused
+// updates their originals in register kr (bit-identical copies).  The
+// leading s_nop covers a DPP read of a VGPR the previous pivot wrote.
+template <int K, int KQ>
+__device__ __forceinline__ void repl_rows_update(double (&Rr)[4], double nw) {
+  double r1 = Rr[1], r2 = Rr[2], r3 = Rr[3];
+  asm(" s_nop 1\n"
+      ".if %[kq] < 1\n v_fmac_f64_dpp %[r1], %[r1], %[nw] row_newbcast:%[k] row_mask:0xf bank_mask:0xf\n .endif\n"
+      ".if %[kq] < 2\n v_fmac_f64_dpp %[r2], %[r2], %[nw] row_newbcast:%[k] row_mask:0xf bank_mask:0xf\n .endif\n"
+      ".if %[kq] < 3\n v_fmac_f64_dpp %[r3], %[r3], %[nw] row_newbcast:%[k] row_mask:0xf bank_mask:0xf\n .endif\n"
+      : [r1] "+v"(r1), [r2] "+v"(r2), [r3] "+v"(r3)
+      : [nw] "v"(nw), [k] "i"(K), [kq] "i"(KQ));
+  Rr[1] = r1; Rr[2] = r2; Rr[3] = r3;
+}
+
+// REPL (the latency kernel): the four rows of each sub-panel are broadcast to
+// every 16-lane row once, when the sub-panel starts (4 ds_bpermute pairs in
+// flight together), and kept up to date by repl_rows_update, so no pivot
+// waits on a ds_bpermute round trip: 6 more DPP multiply-adds per sub-panel
+// for a shorter dependent chain.  Same values bit for bit.
+template <int NB, int BB, bool RL, bool REPL = false>
 __device__ __forceinline__ void diag_factor_2l(v4d& D, v4d& E, double (&rsr)[4], int q, int c, LogAcc& ldet,
                                                bool& ok, int klim) {
   constexpr bool LASTR = RL && BB == NB - 1;          // block row holding the residual
@@ -717,6 +738,10 @@ __device__ __forceinline__ void diag_factor_2l(v4d& D, v4d& E, double (&rsr)[4],
   static_for<0, 4>([&](auto KR) {
     constexpr int kr = decltype(KR)::value;
     constexpr int nk = (LASTR && kr == 3) ? 3 : 4;   // the r column is not pivoted
+    double Rr[4];
+    if constexpr (REPL) {
+      static_for<0, 4>([&](auto J) { Rr[decltype(J)::value] = __shfl(D[kr], 16 * decltype(J)::value + c); });
+    }
     static_for<0, nk>([&](auto KQc) {
       constexpr int kq = decltype(KQc)::value;
       constexpr int k = 4 * kr + kq;
@@ -724,11 +749,12 @@ __device__ __forceinline__ void diag_factor_2l(v4d& D, v4d& E, double (&rsr)[4],
         if (k >= klim) return;                         // wave-uniform: pad pivots
       }
       constexpr bool doe = !LASTR && k < 15;
-      const double xk = __shfl(D[kr], 16 * kq + c);    // A[k][c]
-      const double d = readlane_d(D[kr], 16 * kq + k);
+      const double xk = REPL ? Rr[kq] : __shfl(D[kr], 16 * kq + c);    // A[k][c]
+      const double d = REPL ? readlane_d(Rr[kq], k) : readlane_d(D[kr], 16 * kq + k);
       const double nw = div_fast(-xk, d);
       const double nwm = (doe && c > k) ? nw : 0.0;
       pivot_fused<k, kr, kq, doe, kq == 0, false>(D, E, nw, nwm);
+      if constexpr (REPL && kq < 3) repl_rows_update<k, kq>(Rr, nw);
     });
     // sub-panel kr done: lane (q, c) takes the pivot of row 4 kr + q (lane
     // (q, 4 kr + q)): log-det, positivity, row scale; U_s = D_s^-1/2 V_s and
@@ -1276,12 +1302,12 @@ int launch_chol_small(int mode, int nb, const CholJob* jobs, int B, long long u0
 int launch_chol_big_nb(int nb, const CholJob* jobs, int B, long long u0, long long n, int b_off,
                        const double* theta, int ldth, double* units, double* scr, long long cap, hipStream_t st);
 // latency form for small batches (chol_lat.hip): one 4-wave workgroup per
-// unit of units [0, P B); theta and out may be host-mapped pinned memory; the
-// last workgroup folds the unit terms into out[B] and re-zeroes *counter.
+// unit of units [0, P B); theta and host_units may be host-mapped pinned
+// memory; every unit term goes to units[p B + b] and host_units[p B + b].
 // Returns 1 if nb has no latency kernel (caller uses the batched path).
 constexpr int LAT_NB_MAX = 8;
 int launch_chol_lat(int nb, const CholJob* jobs, int B, int P, const double* theta, int ldth, double* units,
-                    double* out, unsigned* counter, hipStream_t st, bool stamp = false);
+                    double* host_units, hipStream_t st, bool stamp = false);
 // keep_out: pulsar-major kept blocks, keep_bs samples per pulsar (see chol_mfma_kernel KEEP)
 int launch_partial_nb(int nb, int keep, const CholJob* jobs, int B, long long u0, long long n,
                       const double* theta, int ldth, double* units, double* keep_out, int keep_bs, hipStream_t st);

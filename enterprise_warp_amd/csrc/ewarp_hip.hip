@@ -1199,10 +1199,8 @@ struct DevCtx {
   std::vector<Graph> graphs;
   long long graph_clock = 0;
   // latency path of small single-device batches (chol_lat.hip): every pulsar
-  // has the same reduced block count lat_nb <= LAT_NB_MAX (0: not eligible);
-  // lat_ctr = the kernel's finished-unit counter (zero between calls)
+  // has the same reduced block count lat_nb <= LAT_NB_MAX (0: not eligible)
   int lat_nb = 0;
-  unsigned* d_lat_ctr = nullptr;
 };
 
 namespace {
@@ -2002,11 +2000,7 @@ int create_ctx(const ewh_pta_desc* d, const std::vector<ProjCoef>& proj, int dev
     int nb = h->psr[0].fx_nb;
     for (const auto& ps : h->psr)
       if (ps.fx_nb != nb) nb = 0;
-    if (nb >= 1 && nb <= LAT_NB_MAX) {
-      if ((rc = dalloc(h, &h->d_lat_ctr, 1))) return bail(rc);
-      EWH_HIP(hipMemset(h->d_lat_ctr, 0, sizeof(unsigned)));
-      h->lat_nb = nb;
-    }
+    if (nb >= 1 && nb <= LAT_NB_MAX) h->lat_nb = nb;
   }
   *out = h;
   return 0;
@@ -2340,9 +2334,9 @@ int lnl_batch_single(ewh_handle* H, DevCtx* h, int B, double* out_host) {
   EWH_HIP(hipSetDevice(h->device));
   if ((rc = ensure_pinned(&H->h_out, &H->h_out_cap, (size_t)B))) return rc;
   if (h->lat_nb > 0 && B <= LAT_B_MAX && (h->kernel_mode == 0 || h->kernel_mode == 22)) {
-    // latency path: one launch reads theta from the pinned staging, folds
-    // the unit terms and writes lnL to pinned memory (chol_lat.hip)
-    if ((rc = ensure_units(h, B))) return rc;
+    // latency path: one launch reads theta from the pinned staging and writes
+    // the unit terms to pinned memory (chol_lat.hip); the host folds them
+    if ((rc = ensure_units(h, B)) || (rc = ensure_pinned(&H->h_out, &H->h_out_cap, (size_t)h->P * B))) return rc;
     // device addresses of the pinned staging (looked up again only after a reallocation)
     if (H->lat_th_host != H->h_theta) {
       EWH_HIP(hipHostGetDevicePointer((void**)&H->lat_th_dev, H->h_theta, 0));
@@ -2354,11 +2348,16 @@ int lnl_batch_single(ewh_handle* H, DevCtx* h, int B, double* out_host) {
     }
     double *th_dev = H->lat_th_dev, *out_dev = H->lat_out_dev;
     if ((rc = launch_chol_lat(h->lat_nb, h->d_jobs_fixed, B, h->P, th_dev, h->n_param, h->d_units, out_dev,
-                              h->d_lat_ctr, h->stream, h->kernel_mode == 22)) < 0)
+                              h->stream, h->kernel_mode == 22)) < 0)
       return rc;
     if (rc == 0) {
       EWH_HIP(hipStreamSynchronize(h->stream));
-      std::memcpy(out_host, H->h_out, sizeof(double) * B);
+      // lnL_b = sum over pulsars in pulsar order (reduce_units_kernel's fold)
+      for (int b = 0; b < B; ++b) {
+        double s = 0.0;
+        for (int p = 0; p < h->P; ++p) s += H->h_out[(size_t)p * B + b];
+        out_host[b] = s;
+      }
       H->last_split.assign(1, {0, (long long)H->P * B});
       H->last_B = B;
       h->last_B = B;

@@ -396,10 +396,27 @@ class Engine:
         self.h = h
         self.n_slots = [len(L["slots"]) for L in lay]
         del keep
+        # sampler-sized calls (one theta per call: PTMCMC / bilby) go through
+        # persistent buffers whose addresses are bound once -- building two
+        # ctypes pointers per call costs ~5 us, a tenth of the call
+        self._small = np.empty((self.SMALL_B, max(1, self.n_param)))
+        self._small_out = np.empty(self.SMALL_B)
+        self._small_fn = C.CFUNCTYPE(C.c_int, C.c_void_p, C.c_void_p, C.c_int32, C.c_void_p)(
+            ("ewh_lnl_batch", self.lib))
+        self._small_args = (self.h, self._small.ctypes.data, self._small_out.ctypes.data)
+
+    SMALL_B = 8
 
     def lnl_batch(self, theta):
         theta = np.ascontiguousarray(theta, dtype=float)
         B = theta.shape[0]
+        if B <= self.SMALL_B and self.n_param > 0:
+            self._small[:B] = theta
+            h, tp, op = self._small_args
+            rc = self._small_fn(h, tp, B, op)
+            if rc:
+                _lib.check(rc)
+            return self._small_out[:B].copy()
         out = np.empty(B)
         _lib.check(self.lib.ewh_lnl_batch(self.h, _as_ptr(theta, C.c_double), B, _as_ptr(out, C.c_double)))
         return out

@@ -18,7 +18,7 @@ ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 sys.path.insert(0, ROOT)
 os.environ.setdefault("EWARP_HIP_LIB", os.path.join(ROOT, "enterprise_warp_amd", "libewarp_hip_dev.so"))
 WG, NS = 64, 16
-NAMES = {0: "start", 1: "theta staged", 2: "phi^-1 ready", 10: "factorised", 11: "unit term", 12: "end"}
+NAMES = {0: "start", 1: "theta staged", 2: "phi^-1 ready", 10: "factorised", 11: "unit term",}
 
 
 def main():
