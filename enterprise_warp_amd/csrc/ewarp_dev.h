@@ -722,6 +722,13 @@ __device__ __forceinline__ void repl_rows_update(double (&Rr)[4], double nw) {
 // flight together), and kept up to date by repl_rows_update, so no pivot
 // waits on a ds_bpermute round trip: 6 more DPP multiply-adds per sub-panel
 // for a shorter dependent chain.  Same values bit for bit.
+// The pivot d = A[k][k] is read by two v_readlane_b32 from the register
+// itself, in parallel with the ds_bpermute that broadcasts row k.  (Round 3
+// A/B, profiles/r03e/chol_ab.log: taking d from the broadcast row by one
+// v_mov_b64_dpp -- one instruction less per pivot -- put the bpermute's
+// latency in front of the reciprocal: 3.70 vs 3.65 ms per launch; masking
+// only the high dword of the E multiplier -- one v_cndmask_b32 less -- 3.70
+// ms.  Neither is kept.)
 template <int NB, int BB, bool RL, bool REPL = false>
 __device__ __forceinline__ void diag_factor_2l(v4d& D, v4d& E, double (&rsr)[4], int q, int c, LogAcc& ldet,
                                                bool& ok, int klim) {
