@@ -27,6 +27,8 @@
 #include "ewarp_dev.h"
 #include "ewarp_desc.h"
 
+#include <atomic>
+#include <chrono>
 #include <map>
 
 namespace ewh_dev {
@@ -2238,8 +2240,10 @@ int ensure_pinned(double** p, size_t* cap, size_t need) {
   if (*p) (void)hipHostFree(*p);
   *p = nullptr;
   *cap = 0;
+  // coherent: the latency kernel's stores to it are visible to a spinning
+  // host thread before the launch completes (and its theta reads bypass L2)
   hipError_t e = hipHostMalloc((void**)p, std::max<size_t>(need, 1) * sizeof(double),
-                               hipHostMallocPortable | hipHostMallocMapped);
+                               hipHostMallocPortable | hipHostMallocMapped | hipHostMallocCoherent);
   if (e != hipSuccess) return set_err(EWH_E_NOMEM, std::string("hipHostMalloc: ") + hipGetErrorString(e));
   *cap = need;
   return 0;
@@ -2327,6 +2331,7 @@ int lnl_batch_corr_pulsars(ewh_handle* H, int B, double* out_host) {
 // One device: replay the captured graph of this batch size when there is one;
 // otherwise run the batch eagerly (that also sizes every scratch buffer) and
 // capture the same sequence for the next call.
+constexpr uint64_t LAT_SENTINEL = 0x7ff4dead0ebeef01ull;   // a NaN no kernel writes
 constexpr int LAT_B_MAX = 8;    // batches up to this size take the latency kernel (profiles/r03c/latency.log: B = 16 is faster batched)
 
 int lnl_batch_single(ewh_handle* H, DevCtx* h, int B, double* out_host) {
@@ -2347,11 +2352,38 @@ int lnl_batch_single(ewh_handle* H, DevCtx* h, int B, double* out_host) {
       H->lat_out_host = H->h_out;
     }
     double *th_dev = H->lat_th_dev, *out_dev = H->lat_out_dev;
+    // every unit term lands in pinned memory; the host waits for them by
+    // spinning on a sentinel (a NaN payload the kernel never writes: its
+    // terms are finite or -inf) instead of a stream synchronisation, whose
+    // wake-up is a sizeable share of a ~30 us call.  Every workgroup reads
+    // theta before it writes its term, so the staging is free once all terms
+    // are in; a launch error or a stall falls back to the stream (2 s)
+    const size_t nu = (size_t)h->P * B;
+    volatile uint64_t* hu = reinterpret_cast<volatile uint64_t*>(H->h_out);
+    for (size_t i = 0; i < nu; ++i) hu[i] = LAT_SENTINEL;
     if ((rc = launch_chol_lat(h->lat_nb, h->d_jobs_fixed, B, h->P, th_dev, h->n_param, h->d_units, out_dev,
                               h->stream, h->kernel_mode == 22)) < 0)
       return rc;
     if (rc == 0) {
-      EWH_HIP(hipStreamSynchronize(h->stream));
+      const auto t0 = std::chrono::steady_clock::now();
+      size_t seen = 0;
+      for (long spins = 0;; ++spins) {
+        while (seen < nu && hu[seen] != LAT_SENTINEL) ++seen;
+        if (seen == nu) break;
+        if ((spins & 4095) == 4095) {
+          const hipError_t q = hipStreamQuery(h->stream);
+          if (q != hipSuccess && q != hipErrorNotReady)
+            return set_err(EWH_E_HIP, std::string("chol_lat_kernel: ") + hipGetErrorString(q));
+          if (std::chrono::steady_clock::now() - t0 > std::chrono::seconds(2)) {
+            EWH_HIP(hipStreamSynchronize(h->stream));
+            for (seen = 0; seen < nu && hu[seen] != LAT_SENTINEL; ++seen) {
+            }
+            if (seen != nu) return set_err(EWH_E_HIP, "chol_lat_kernel: unit terms missing after the launch");
+            break;
+          }
+        }
+      }
+      std::atomic_thread_fence(std::memory_order_acquire);
       // lnL_b = sum over pulsars in pulsar order (reduce_units_kernel's fold)
       for (int b = 0; b < B; ++b) {
         double s = 0.0;
