@@ -189,6 +189,45 @@ def secondary_configs(dev, steps=5):
     return out
 
 
+def secondary_c5(dev, steps=3, steps_one=20):
+    """BASELINE config 5 (100 psr x 20k TOAs, Hellings-Downs GWB, fixed white
+    noise) on this GPU: evals/s of 512-proposal batches, and the latency of
+    one proposal (the right-looking dense factorisation), HIP events around
+    ewh_lnl_units_device.  Algorithmic work as main_c5."""
+    import torch
+    from enterprise_warp_amd import synth
+    cfg = synth.config_c5()
+    pta = cfg.pta
+    eng = pta.engine(device=dev.index)
+    P = len(pta.signal_collections)
+    st = torch.cuda.current_stream(dev)
+    res = {}
+    for B, n in ((cfg.B, steps), (1, steps_one)):
+        X = synth.prior_draws(pta, B, cfg.theta_seed)
+        th = torch.from_numpy(X).to(dev)
+        out = torch.zeros(B, dtype=torch.float64, device=dev)
+        eng.lnl_units_device(th.data_ptr(), B, 0, P * B, out.data_ptr(), st.cuda_stream)
+        torch.cuda.synchronize(dev)
+        a, b = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        a.record(st)
+        for _ in range(n):
+            eng.lnl_units_device(th.data_ptr(), B, 0, P * B, out.data_ptr(), st.cuda_stream)
+        b.record(st)
+        torch.cuda.synchronize(dev)
+        ms = a.elapsed_time(b) / n
+        res[f"B{B}"] = {"ms_per_batch": ms, "evals_per_s": B / (ms * 1e-3),
+                        "finite_fraction": float(np.mean(np.isfinite(out.cpu().numpy())))}
+    nc = pta.common_layout()["n_col"]
+    m = np.array([c.T.shape[1] for c in pta.signal_collections])
+    f = float(np.sum(m ** 3 / 3.0)) + (P * nc + 1) ** 3 / 3.0
+    res[f"B{cfg.B}"]["fp64_mfma_frac"] = f * cfg.B / (res[f"B{cfg.B}"]["ms_per_batch"] * 1e-3) / 1e12 / \
+        FP64_MFMA_PEAK_TFLOPS
+    res["note"] = ("config 5 at its stated size, prior draws; B1 = one PTMCMC proposal (right-looking dense "
+                   "Sigma_c); algorithmic work per sample sum_a m_a^3/3 + (P n_gw + 1)^3 / 3")
+    pta._drop_engine()
+    return res
+
+
 def kernel_sources_sha():
     """sha256 of the sources of the factorisation kernel (ewarp_dev.h and its
     instantiating translation unit): ties a committed PMC profile to this tree."""
@@ -238,7 +277,8 @@ def main():
     ap.add_argument("--cpu-procs", type=int, default=None, help="default: every usable core (affinity / cgroup quota)")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-latency", action="store_true")
-    ap.add_argument("--no-secondary", action="store_true", help="skip the C2 / C4 secondary measurements")
+    ap.add_argument("--no-secondary", action="store_true", help="skip the C2 / C4 / C5 secondary measurements")
+    ap.add_argument("--no-c5", action="store_true", help="skip the C5 secondary measurement (~40 s of model build)")
     ap.add_argument("--kernel-mode", type=int, default=0, help="0 auto (MFMA), 1 LDS fallback")
     ap.add_argument("--config", default="c3", choices=["c3", "c5"],
                     help="c3: the headline 45-pulsar CURN batch (default); c5: 100-pulsar HD-correlated PTA")
@@ -382,6 +422,8 @@ def main():
     if rank == 0 and world == 1 and not args.no_secondary:
         pta._drop_engine()
         secondary = secondary_configs(dev)
+        if not args.no_c5:
+            secondary["c5"] = secondary_c5(dev)
     if rank == 0:
         value = B * args.steps / elapsed
         rec = {
