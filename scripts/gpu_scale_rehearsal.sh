@@ -11,7 +11,7 @@ timeout -k 10 300 python -m torch.distributed.run --nnodes=1 --nproc-per-node 2 
 rc=$?
 echo "n2 rc=$rc"; tail -3 gpurun_out/rehearsal_n2.log
 [ $rc -eq 0 ] || exit $rc
-timeout -k 10 300 python bench.py --steps 10 --warmup 2 --verify --no-cpu-baseline --no-latency \
+timeout -k 10 300 python bench.py --steps 10 --warmup 2 --verify --no-cpu-baseline --no-latency --no-secondary \
   > gpurun_out/rehearsal_n1.log 2>&1
 rc=$?
 echo "n1 rc=$rc"; tail -2 gpurun_out/rehearsal_n1.log
