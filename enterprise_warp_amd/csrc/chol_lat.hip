@@ -33,7 +33,41 @@
 namespace ewh_dev {
 namespace {
 
-constexpr int lat_owner(int i, int j) { return (i + j) & 3; }
+// Block (i, j) -> wave.  LAT_MAP (the default): per-NB maps annealed by
+// scripts/lat_owner_search.py against the panel-time model fitted to the
+// round-3 stamps (profiles/r03f/lat_stamps_b1.log): the owner of the next
+// diagonal block -- which runs that block's pivot chain (lookahead) before
+// its trailing updates -- gets a light share of the trailing blocks, so the
+// chain, not that wave's MFMA queue, sets the panel time (model for NB = 8:
+// 40.4 k -> 34.2 k cycles over the seven panels).  LAT_VAR_R3 (dev A/B):
+// the round-3 map (i + j) mod 4 and prologue.
+constexpr unsigned char LAT_MAP[9][8][8] = {{},
+  {{0,0,0,0,0,0,0,0}, {0,0,0,0,0,0,0,0}, {0,0,0,0,0,0,0,0}, {0,0,0,0,0,0,0,0}, {0,0,0,0,0,0,0,0}, {0,0,0,0,0,0,0,0}, {0,0,0,0,0,0,0,0}, {0,0,0,0,0,0,0,0}},
+  {{0,0,0,0,0,0,0,0}, {0,2,0,0,0,0,0,0}, {0,0,0,0,0,0,0,0}, {0,0,0,0,0,0,0,0}, {0,0,0,0,0,0,0,0}, {0,0,0,0,0,0,0,0}, {0,0,0,0,0,0,0,0}, {0,0,0,0,0,0,0,0}},
+  {{2,2,3,0,0,0,0,0}, {0,0,1,0,0,0,0,0}, {0,0,1,0,0,0,0,0}, {0,0,0,0,0,0,0,0}, {0,0,0,0,0,0,0,0}, {0,0,0,0,0,0,0,0}, {0,0,0,0,0,0,0,0}, {0,0,0,0,0,0,0,0}},
+  {{0,0,3,1,0,0,0,0}, {0,0,2,3,0,0,0,0}, {0,0,3,2,0,0,0,0}, {0,0,0,1,0,0,0,0}, {0,0,0,0,0,0,0,0}, {0,0,0,0,0,0,0,0}, {0,0,0,0,0,0,0,0}, {0,0,0,0,0,0,0,0}},
+  {{1,2,3,0,1,0,0,0}, {0,2,3,1,0,0,0,0}, {0,0,1,0,3,0,0,0}, {0,0,0,3,0,0,0,0}, {0,0,0,0,0,0,0,0}, {0,0,0,0,0,0,0,0}, {0,0,0,0,0,0,0,0}, {0,0,0,0,0,0,0,0}},
+  {{0,0,0,1,3,1,0,0}, {0,1,3,2,2,3,0,0}, {0,0,1,2,0,3,0,0}, {0,0,0,0,2,3,0,0}, {0,0,0,0,2,3,0,0}, {0,0,0,0,0,3,0,0}, {0,0,0,0,0,0,0,0}, {0,0,0,0,0,0,0,0}},
+  {{1,1,3,1,2,0,3,0}, {0,1,0,2,3,0,2,0}, {0,0,1,3,0,2,0,0}, {0,0,0,1,0,3,2,0}, {0,0,0,0,3,2,0,0}, {0,0,0,0,0,0,2,0}, {0,0,0,0,0,0,2,0}, {0,0,0,0,0,0,0,0}},
+  {{2,3,1,1,0,2,0,3}, {0,1,0,2,2,0,3,3}, {0,0,1,2,3,0,0,2}, {0,0,0,1,3,3,0,0}, {0,0,0,0,1,2,0,3}, {0,0,0,0,0,0,3,2}, {0,0,0,0,0,0,3,2}, {0,0,0,0,0,0,0,2}},
+};
+constexpr int LAT_VAR_DEFAULT = 0, LAT_VAR_MAP_ONLY = 1, LAT_VAR_R3 = 2;
+template <int NB, int VAR>
+constexpr int lat_owner(int i, int j) { return VAR == LAT_VAR_R3 ? (i + j) & 3 : LAT_MAP[NB][i][j]; }
+// wave w owns a block (bb, j > bb) of block row bb
+template <int NB, int VAR>
+constexpr bool lat_row_owned(int w, int bb) {
+  for (int j = bb + 1; j < NB; ++j)
+    if (lat_owner<NB, VAR>(bb, j) == w) return true;
+  return false;
+}
+// wave w owns a block (i, j >= i) of row i that panel bb updates after the lookahead block
+template <int NB, int VAR>
+constexpr bool lat_trail_owned(int w, int bb, int i) {
+  for (int j = i; j < NB; ++j)
+    if (lat_owner<NB, VAR>(i, j) == w && !(i == bb + 1 && j == bb + 1)) return true;
+  return false;
+}
 
 #ifdef EWH_DEV
 // phase stamps (dev mode 22): s_memtime per wave of the first LAT_STAMP_WG
@@ -57,6 +91,7 @@ struct LatLds {
   double phinv[16 * NB];
   double phs[16 * NB];
   double ths[STAGE_THETA_MAX];
+  double thr[STAGE_THETA_MAX];   // the whole theta row (prefetched prologue)
   double E[4][64];          // E = L^-T of the current diagonal block (register r, lane)
   double R[4][64];          // its row scales D^-1/2 (register r, lane)
   double U[NB][4][64];      // U blocks (bb, j) of the current block row
@@ -74,9 +109,10 @@ __device__ __forceinline__ v4d lds_get(const double (*src)[64], int lane) {
   return v;
 }
 
-template <int NB, int W, bool STAMP>
+template <int NB, int W, bool STAMP, int VAR>
 __device__ __forceinline__ void lat_wave(LatLds<NB>& S, const CholJob& J, const int* tidx, const double* __restrict__ A,
-                                         const double* th, int ldth, int lane, LogAcc& ldet, bool& ok) {
+                                         const double* th, int ldth, const double (&tv)[2], int lane, LogAcc& ldet,
+                                         bool& ok) {
   constexpr int LD = 16 * NB;
   const int tid = 64 * W + lane;
   const int q = lane >> 4, c = lane & 15;
@@ -93,7 +129,7 @@ __device__ __forceinline__ void lat_wave(LatLds<NB>& S, const CholJob& J, const 
     constexpr int i = decltype(I)::value;
     static_for<i, NB>([&](auto JJ) {
       constexpr int j = decltype(JJ)::value;
-      if constexpr (lat_owner(i, j) == W) {
+      if constexpr (lat_owner<NB, VAR>(i, j) == W) {
         static_for<0, 4>([&](auto R) {
           constexpr int r = decltype(R)::value;
           C[i][j][r] = A[(long long)(16 * i + q + 4 * r) * LD + 16 * j + c];
@@ -101,6 +137,48 @@ __device__ __forceinline__ void lat_wave(LatLds<NB>& S, const CholJob& J, const 
       }
     });
   });
+  constexpr bool PRE = VAR == LAT_VAR_DEFAULT;
+  static_assert(LD <= 256 && 2 * 256 >= STAGE_THETA_MAX, "one column / record per thread; theta row in two loads");
+  if (PRE && J.urec != nullptr && ldth <= STAGE_THETA_MAX) {
+    // the theta row arrived in tv (read at kernel entry); this thread's
+    // spectrum record, its column's record index and its compact theta index
+    // are loaded before the row is waited for, so their latency hides under
+    // the PCIe round trip instead of following it
+    const bool hasr = tid < J.nu;
+    URec R;
+    if (hasr) R = J.urec[tid];
+    const int ur = tid < J.mreal ? J.urep[tid] : -1;
+    const int ti = (compact && tid < J.ntidx) ? tidx[tid] : 0;
+    // (S.ths holds what the records index: the compact entries, gathered from
+    // the row in S.thr, or the row itself)
+    double* row = compact ? S.thr : S.ths;
+    if (tid < ldth) row[tid] = tv[0];
+    if (tid + 256 < ldth) row[tid + 256] = tv[1];
+    __syncthreads();
+    if (compact) {
+      if (tid < J.ntidx) S.ths[tid] = S.thr[ti];
+      __syncthreads();
+    }
+    LAT_STAMP(1)
+    const double* tp = S.ths;
+    if (hasr) {
+      double ph = 0.0;
+      static_for<0, URec::NE>([&](auto E) {   // (constant indices: R stays in registers)
+        if (decltype(E)::value < R.ne) ph += spec_phi_body(R.e[decltype(E)::value], tp);
+      });
+      S.phs[tid] = ph;
+    }
+    __syncthreads();
+    if (tid < LD) {
+      double pi = 0.0;
+      if (ur >= 0) {
+        const double ph = S.phs[ur];
+        pi = 1.0 / ph;
+        ldet.add(ph);
+      }
+      S.phinv[tid] = pi;
+    }
+  } else {
   if (stage) {
     if (compact) {
       if (tid < J.ntidx) S.ths[tid] = th[tidx[tid]];   // (tidx: the job in global memory)
@@ -155,11 +233,12 @@ __device__ __forceinline__ void lat_wave(LatLds<NB>& S, const CholJob& J, const 
       S.phinv[a] = pi;
     }
   }
+  }
   __syncthreads();
   LAT_STAMP(2)
   static_for<0, NB>([&](auto I) {
     constexpr int i = decltype(I)::value;
-    if constexpr (lat_owner(i, i) == W) {
+    if constexpr (lat_owner<NB, VAR>(i, i) == W) {
       const double pd = S.phinv[16 * i + c];
       static_for<0, 4>([&](auto R) {
         constexpr int r = decltype(R)::value;
@@ -182,28 +261,24 @@ __device__ __forceinline__ void lat_wave(LatLds<NB>& S, const CholJob& J, const 
       if (lane == 0) S.qv = qv;
     }
   };
-  if constexpr (lat_owner(0, 0) == W) factor(std::integral_constant<int, 0>{});
+  if constexpr (lat_owner<NB, VAR>(0, 0) == W) factor(std::integral_constant<int, 0>{});
   static_for<0, NB - 1>([&](auto BBc) {
     constexpr int bb = decltype(BBc)::value;
     __syncthreads();                                       // E, scales of panel bb
     LAT_STAMP(3 + bb)
-    constexpr bool row_owned = [] {
-      for (int j = bb + 1; j < NB; ++j)
-        if (lat_owner(bb, j) == W) return true;
-      return false;
-    }();
+    constexpr bool row_owned = lat_row_owned<NB, VAR>(W, bb);
     if constexpr (row_owned) {
-      if constexpr (lat_owner(bb, bb) != W) {
+      if constexpr (lat_owner<NB, VAR>(bb, bb) != W) {
         E = lds_get(S.E, lane);
         static_for<0, 4>([&](auto R) { rsr[decltype(R)::value] = S.R[decltype(R)::value][lane]; });
       }
       static_for<bb + 1, NB>([&](auto JJ) {
         constexpr int j = decltype(JJ)::value;
-        if constexpr (lat_owner(bb, j) == W) row_v_2l(E, C[bb][j]);
+        if constexpr (lat_owner<NB, VAR>(bb, j) == W) row_v_2l(E, C[bb][j]);
       });
       static_for<bb + 1, NB>([&](auto JJ) {
         constexpr int j = decltype(JJ)::value;
-        if constexpr (lat_owner(bb, j) == W) {
+        if constexpr (lat_owner<NB, VAR>(bb, j) == W) {
           static_for<0, 4>([&](auto R) { C[bb][j][decltype(R)::value] *= rsr[decltype(R)::value]; });
           lds_put(S.U[j], C[bb][j], lane);
         }
@@ -212,27 +287,23 @@ __device__ __forceinline__ void lat_wave(LatLds<NB>& S, const CholJob& J, const 
     __syncthreads();                                       // U blocks of row bb
     auto ublk = [&](auto II) -> v4d {
       constexpr int i = decltype(II)::value;
-      if constexpr (lat_owner(bb, i) == W) return C[bb][i];
+      if constexpr (lat_owner<NB, VAR>(bb, i) == W) return C[bb][i];
       else return lds_get(S.U[i], lane);
     };
     // lookahead: the next diagonal block first, then its panel
-    if constexpr (lat_owner(bb + 1, bb + 1) == W) {
+    if constexpr (lat_owner<NB, VAR>(bb + 1, bb + 1) == W) {
       const v4d u = ublk(std::integral_constant<int, bb + 1>{});
       syrk_update(C[bb + 1][bb + 1], u, u);
       factor(std::integral_constant<int, bb + 1>{});
     }
     static_for<bb + 1, NB>([&](auto II) {
       constexpr int i = decltype(II)::value;
-      constexpr bool any = [] {
-        for (int j = i; j < NB; ++j)
-          if (lat_owner(i, j) == W && !(i == bb + 1 && j == bb + 1)) return true;
-        return false;
-      }();
+      constexpr bool any = lat_trail_owned<NB, VAR>(W, bb, i);
       if constexpr (any) {
         const v4d ui = ublk(II);
         static_for<i, NB>([&](auto JJ) {
           constexpr int j = decltype(JJ)::value;
-          if constexpr (lat_owner(i, j) == W && !(i == bb + 1 && j == bb + 1)) {
+          if constexpr (lat_owner<NB, VAR>(i, j) == W && !(i == bb + 1 && j == bb + 1)) {
             if constexpr (j == i) syrk_update(C[i][j], ui, ui);
             else syrk_update(C[i][j], ui, ublk(JJ));
           }
@@ -243,7 +314,7 @@ __device__ __forceinline__ void lat_wave(LatLds<NB>& S, const CholJob& J, const 
   LAT_STAMP(10)
 }
 
-template <int NB, bool STAMP>
+template <int NB, bool STAMP, int VAR>
 __global__ __launch_bounds__(256) void chol_lat_kernel(const CholJob* __restrict__ jobs, int B, int P,
                                                        const double* theta, int ldth, double* __restrict__ out_units,
                                                        double* host_units) {
@@ -252,16 +323,28 @@ __global__ __launch_bounds__(256) void chol_lat_kernel(const CholJob* __restrict
   (void)P;
   const int u = blockIdx.x;
   const int p = u / B, b = u % B;
+  // theta first: the whole row when it fits the LDS stage, read from pinned
+  // host memory before the job record, so its PCIe round trip overlaps the
+  // record and block loads (the round-3 prologue read the compact entries
+  // after the record's index list had arrived: two latencies in series)
+  double tv[2] = {0.0, 0.0};
+  if constexpr (VAR == LAT_VAR_DEFAULT) {
+    const double* t0 = theta + (long long)b * ldth;
+    if (ldth <= STAGE_THETA_MAX) {
+      if (tid < ldth) tv[0] = t0[tid];
+      if (tid + 256 < ldth) tv[1] = t0[tid + 256];
+    }
+  }
   const CholJob J = jobs[p];
   const double* A = J.mats + (long long)b * J.mstride;
   const double* th = theta + (long long)b * ldth;
   LogAcc ldet;
   bool ok = true;
   switch (w) {
-    case 0: lat_wave<NB, 0, STAMP>(S, J, jobs[p].tidx, A, th, ldth, lane, ldet, ok); break;
-    case 1: lat_wave<NB, 1, STAMP>(S, J, jobs[p].tidx, A, th, ldth, lane, ldet, ok); break;
-    case 2: lat_wave<NB, 2, STAMP>(S, J, jobs[p].tidx, A, th, ldth, lane, ldet, ok); break;
-    default: lat_wave<NB, 3, STAMP>(S, J, jobs[p].tidx, A, th, ldth, lane, ldet, ok); break;
+    case 0: lat_wave<NB, 0, STAMP, VAR>(S, J, jobs[p].tidx, A, th, ldth, tv, lane, ldet, ok); break;
+    case 1: lat_wave<NB, 1, STAMP, VAR>(S, J, jobs[p].tidx, A, th, ldth, tv, lane, ldet, ok); break;
+    case 2: lat_wave<NB, 2, STAMP, VAR>(S, J, jobs[p].tidx, A, th, ldth, tv, lane, ldet, ok); break;
+    default: lat_wave<NB, 3, STAMP, VAR>(S, J, jobs[p].tidx, A, th, ldth, tv, lane, ldet, ok); break;
   }
   const double lw = wave_sum(ldet.value());
   const bool okw = __all(ok);
@@ -280,14 +363,14 @@ __global__ __launch_bounds__(256) void chol_lat_kernel(const CholJob* __restrict
   LAT_STAMP(12)
 }
 
-template <bool STAMP>
+template <bool STAMP, int VAR>
 int launch_chol_lat_t(int nb, const CholJob* jobs, int B, int P, const double* theta, int ldth, double* units,
                       double* host_units, hipStream_t st) {
   const dim3 grid((unsigned)(P * B)), block(256);
 #define EWH_LAT_CASE(N)                                                                                          \
   case N:                                                                                                        \
-    hipLaunchKernelGGL(HIP_KERNEL_NAME(chol_lat_kernel<N, STAMP>), grid, block, 0, st, jobs, B, P, theta, ldth, \
-                       units, host_units);                                                                       \
+    hipLaunchKernelGGL(HIP_KERNEL_NAME(chol_lat_kernel<N, STAMP, VAR>), grid, block, 0, st, jobs, B, P, theta,  \
+                       ldth, units, host_units);                                                                 \
     break;
   switch (nb) {
     EWH_LAT_CASE(1) EWH_LAT_CASE(2) EWH_LAT_CASE(3) EWH_LAT_CASE(4)
@@ -302,12 +385,16 @@ int launch_chol_lat_t(int nb, const CholJob* jobs, int B, int P, const double* t
 }  // namespace
 
 int launch_chol_lat(int nb, const CholJob* jobs, int B, int P, const double* theta, int ldth, double* units,
-                    double* host_units, hipStream_t st, bool stamp) {
+                    double* host_units, hipStream_t st, bool stamp, int var) {
 #ifdef EWH_DEV
-  if (stamp) return launch_chol_lat_t<true>(nb, jobs, B, P, theta, ldth, units, host_units, st);
+  if (stamp) return launch_chol_lat_t<true, LAT_VAR_DEFAULT>(nb, jobs, B, P, theta, ldth, units, host_units, st);
+  if (var == LAT_VAR_MAP_ONLY)
+    return launch_chol_lat_t<false, LAT_VAR_MAP_ONLY>(nb, jobs, B, P, theta, ldth, units, host_units, st);
+  if (var == LAT_VAR_R3) return launch_chol_lat_t<false, LAT_VAR_R3>(nb, jobs, B, P, theta, ldth, units, host_units, st);
 #endif
   (void)stamp;
-  return launch_chol_lat_t<false>(nb, jobs, B, P, theta, ldth, units, host_units, st);
+  (void)var;
+  return launch_chol_lat_t<false, LAT_VAR_DEFAULT>(nb, jobs, B, P, theta, ldth, units, host_units, st);
 }
 
 #ifdef EWH_DEV

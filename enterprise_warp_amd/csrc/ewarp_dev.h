@@ -1314,7 +1314,7 @@ int launch_chol_big_nb(int nb, const CholJob* jobs, int B, long long u0, long lo
 // Returns 1 if nb has no latency kernel (caller uses the batched path).
 constexpr int LAT_NB_MAX = 8;
 int launch_chol_lat(int nb, const CholJob* jobs, int B, int P, const double* theta, int ldth, double* units,
-                    double* host_units, hipStream_t st, bool stamp = false);
+                    double* host_units, hipStream_t st, bool stamp = false, int var = 0);
 // keep_out: pulsar-major kept blocks, keep_bs samples per pulsar (see chol_mfma_kernel KEEP)
 int launch_partial_nb(int nb, int keep, const CholJob* jobs, int B, long long u0, long long n,
                       const double* theta, int ldth, double* units, double* keep_out, int keep_bs, hipStream_t st);

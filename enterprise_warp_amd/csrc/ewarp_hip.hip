@@ -2338,7 +2338,8 @@ int lnl_batch_single(ewh_handle* H, DevCtx* h, int B, double* out_host) {
   int rc;
   EWH_HIP(hipSetDevice(h->device));
   if ((rc = ensure_pinned(&H->h_out, &H->h_out_cap, (size_t)B))) return rc;
-  if (h->lat_nb > 0 && B <= LAT_B_MAX && (h->kernel_mode == 0 || h->kernel_mode == 22)) {
+  const int km = h->kernel_mode;
+  if (h->lat_nb > 0 && B <= LAT_B_MAX && (km == 0 || km == 22 || km == 24 || km == 25)) {
     // latency path: one launch reads theta from the pinned staging and writes
     // the unit terms to pinned memory (chol_lat.hip); the host folds them
     if ((rc = ensure_units(h, B)) || (rc = ensure_pinned(&H->h_out, &H->h_out_cap, (size_t)h->P * B))) return rc;
@@ -2362,7 +2363,7 @@ int lnl_batch_single(ewh_handle* H, DevCtx* h, int B, double* out_host) {
     volatile uint64_t* hu = reinterpret_cast<volatile uint64_t*>(H->h_out);
     for (size_t i = 0; i < nu; ++i) hu[i] = LAT_SENTINEL;
     if ((rc = launch_chol_lat(h->lat_nb, h->d_jobs_fixed, B, h->P, th_dev, h->n_param, h->d_units, out_dev,
-                              h->stream, h->kernel_mode == 22)) < 0)
+                              h->stream, km == 22, km == 24 ? 1 : km == 25 ? 2 : 0)) < 0)
       return rc;
     if (rc == 0) {
       const auto t0 = std::chrono::steady_clock::now();
