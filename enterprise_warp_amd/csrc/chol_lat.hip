@@ -7,8 +7,8 @@
 // units of C3 occupy 45 of 1024 SIMDs and each is a ~20 us chain of 472 MFMAs
 // and 121 dependent pivots on ONE SIMD.  Here each unit gets a 4-wave
 // workgroup (one CU, four SIMDs).  The 16x16 upper blocks (i, j) are dealt to
-// the waves by (i + j) mod 4, which balances every panel's trailing update;
-// the owner of a diagonal block factors it (diag_factor_2l, the same
+// the waves by LAT_MAP (below), which keeps the owner of each panel's next
+// diagonal block lightly loaded; the owner of a diagonal block factors it (diag_factor_2l, the same
 // two-level panel as the batched kernel) and publishes E = L^-T and the row
 // scales through LDS; every wave applies them to its blocks of the block row
 // (row_v_2l), publishes those U blocks, and takes its trailing updates
@@ -51,7 +51,12 @@ constexpr unsigned char LAT_MAP[9][8][8] = {{},
   {{1,1,3,1,2,0,3,0}, {0,1,0,2,3,0,2,0}, {0,0,1,3,0,2,0,0}, {0,0,0,1,0,3,2,0}, {0,0,0,0,3,2,0,0}, {0,0,0,0,0,0,2,0}, {0,0,0,0,0,0,2,0}, {0,0,0,0,0,0,0,0}},
   {{2,3,1,1,0,2,0,3}, {0,1,0,2,2,0,3,3}, {0,0,1,2,3,0,0,2}, {0,0,0,1,3,3,0,0}, {0,0,0,0,1,2,0,3}, {0,0,0,0,0,0,3,2}, {0,0,0,0,0,0,3,2}, {0,0,0,0,0,0,0,2}},
 };
-constexpr int LAT_VAR_DEFAULT = 0, LAT_VAR_MAP_ONLY = 1, LAT_VAR_R3 = 2;
+// Variants: LAT_VAR_FLOW (the default) -- LAT_MAP, theta at kernel entry, the
+// panel loop as a dataflow over LDS counters (lat_flow); dev A/B only:
+// LAT_VAR_BARRIER -- the same with two block barriers per panel;
+// LAT_VAR_R3 -- the round-3 kernel ((i + j) mod 4, theta after the job record).
+[[maybe_unused]] constexpr int LAT_VAR_FLOW = 0, LAT_VAR_BARRIER = 1, LAT_VAR_R3 = 2;
+constexpr bool lat_pre(int var) { return var != LAT_VAR_R3; }
 template <int NB, int VAR>
 constexpr int lat_owner(int i, int j) { return VAR == LAT_VAR_R3 ? (i + j) & 3 : LAT_MAP[NB][i][j]; }
 // wave w owns a block (bb, j > bb) of block row bb
@@ -67,6 +72,19 @@ constexpr bool lat_trail_owned(int w, int bb, int i) {
   for (int j = i; j < NB; ++j)
     if (lat_owner<NB, VAR>(i, j) == w && !(i == bb + 1 && j == bb + 1)) return true;
   return false;
+}
+template <int NB, int VAR>
+constexpr bool lat_any_trail(int w, int bb) {
+  for (int i = bb + 1; i < NB; ++i)
+    if (lat_trail_owned<NB, VAR>(w, bb, i)) return true;
+  return false;
+}
+// blocks (bb, j > bb) wave w owns
+template <int NB, int VAR>
+constexpr int lat_row_count(int w, int bb) {
+  int n = 0;
+  for (int j = bb + 1; j < NB; ++j) n += lat_owner<NB, VAR>(bb, j) == w;
+  return n;
 }
 
 #ifdef EWH_DEV
@@ -86,19 +104,48 @@ __device__ long long g_lat_stamps[LAT_STAMP_WG * 4 * LAT_STAMP_N];
 #define LAT_STAMP(I)
 #endif
 
+constexpr int LAT_NBUF = 3;
 template <int NB>
 struct LatLds {
   double phinv[16 * NB];
   double phs[16 * NB];
   double ths[STAGE_THETA_MAX];
   double thr[STAGE_THETA_MAX];   // the whole theta row (prefetched prologue)
-  double E[4][64];          // E = L^-T of the current diagonal block (register r, lane)
-  double R[4][64];          // its row scales D^-1/2 (register r, lane)
-  double U[NB][4][64];      // U blocks (bb, j) of the current block row
   double ldet[4];
   int ok[4];
   double qv;
+  // panel k's E = L^-T of the diagonal block, its row scales D^-1/2 and the
+  // U blocks (k, j) of the block row, in buffer k % LAT_NBUF (LAT_VAR_FLOW;
+  // the barrier form uses buffer 0), and the LDS counters the dataflow
+  // waits on instead of block barriers
+  double Ef[LAT_NBUF][4][64];
+  double Rf[LAT_NBUF][4][64];
+  double Uf[LAT_NBUF][NB][4][64];
+  int eflag[NB];            // 1: E and scales of panel k published
+  int ucount[NB];           // U blocks of block row k published
+  int unext[NB];            // 1: U block (k, k + 1) published (the lookahead's operand)
+  int done[NB];             // waves through panel k
+  int stall;                // a wait ran out (never expected): the unit term becomes NaN
 };
+
+// LAT_VAR_FLOW synchronisation through LDS counters: a wave publishes with
+// one workgroup-scope release add by lane 0 (after the wave's own LDS
+// writes), a consumer spins with acquire loads.  Every wait targets data
+// produced earlier in some wave's program order (the panel dependency DAG),
+// and is bounded: a wait that runs out marks the unit (NaN term) and goes on.
+constexpr int LAT_SPIN_MAX = 1 << 22;
+__device__ __forceinline__ void lat_signal(int* f, int add, int lane) {
+  if (lane == 0) __hip_atomic_fetch_add(f, add, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_WORKGROUP);
+}
+__device__ __forceinline__ void lat_wait(int* f, int target, int* stall) {
+  for (int n = 0; __hip_atomic_load(f, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_WORKGROUP) < target; ++n) {
+    if (n >= LAT_SPIN_MAX) {
+      *stall = 1;
+      break;
+    }
+    __builtin_amdgcn_s_sleep(1);
+  }
+}
 
 __device__ __forceinline__ void lds_put(double (*dst)[64], const v4d& v, int lane) {
   static_for<0, 4>([&](auto R) { dst[decltype(R)::value][lane] = v[decltype(R)::value]; });
@@ -107,6 +154,91 @@ __device__ __forceinline__ v4d lds_get(const double (*src)[64], int lane) {
   v4d v;
   static_for<0, 4>([&](auto R) { v[decltype(R)::value] = src[decltype(R)::value][lane]; });
   return v;
+}
+
+// LAT_VAR_FLOW: the panel loop as a dataflow.  Per panel bb a wave (1) forms
+// and publishes its U blocks of block row bb once E_bb is out (the owner of
+// (bb, bb) has it in registers), (2) waits for the whole U row, (3) if it
+// owns (bb+1, bb+1), updates and factors it and publishes E_{bb+1} at once,
+// (4) takes its trailing updates and counts itself through the panel.  No
+// block barrier: a wave with little trailing work runs ahead into the next
+// panel's row V while others finish theirs.  Buffers rotate over LAT_NBUF
+// panels; a writer of buffer k % LAT_NBUF first waits for every wave to be
+// through panel k - LAT_NBUF (its last readers).  Same operations per block
+// in the same order as the barrier form.
+template <int NB, int W, bool STAMP, int VAR>
+__device__ __forceinline__ void lat_flow(LatLds<NB>& S, v4d (&C)[NB][NB], v4d& E, double (&rsr)[4], int q, int c,
+                                         int lane, LogAcc& ldet, bool& ok, int klast) {
+  int* const stall = &S.stall;
+  auto factor = [&](auto BBc) {
+    constexpr int bb = decltype(BBc)::value;
+    diag_factor_2l<NB, bb, true, true>(C[bb][bb], E, rsr, q, c, ldet, ok, klast);
+    if constexpr (bb < NB - 1) {
+      if constexpr (bb >= LAT_NBUF) lat_wait(&S.done[bb - LAT_NBUF], 4, stall);
+      lds_put(S.Ef[bb % LAT_NBUF], E, lane);
+      static_for<0, 4>([&](auto R) { S.Rf[bb % LAT_NBUF][decltype(R)::value][lane] = rsr[decltype(R)::value]; });
+      lat_signal(&S.eflag[bb], 1, lane);
+    } else {
+      const double qv = readlane_d(C[bb][bb][3], 63);
+      if (lane == 0) S.qv = qv;
+    }
+  };
+  if constexpr (lat_owner<NB, VAR>(0, 0) == W) factor(std::integral_constant<int, 0>{});
+  static_for<0, NB - 1>([&](auto BBc) {
+    constexpr int bb = decltype(BBc)::value;
+    constexpr int buf = bb % LAT_NBUF;
+    constexpr int nown = lat_row_count<NB, VAR>(W, bb);
+    if constexpr (nown > 0) {
+      if constexpr (lat_owner<NB, VAR>(bb, bb) != W) {
+        lat_wait(&S.eflag[bb], 1, stall);
+        E = lds_get(S.Ef[buf], lane);
+        static_for<0, 4>([&](auto R) { rsr[decltype(R)::value] = S.Rf[buf][decltype(R)::value][lane]; });
+      }
+      LAT_STAMP(3 + bb)
+      if constexpr (bb >= LAT_NBUF) lat_wait(&S.done[bb - LAT_NBUF], 4, stall);
+      // block by block, (bb, bb + 1) first: the next diagonal block's owner
+      // waits on that one alone
+      static_for<bb + 1, NB>([&](auto JJ) {
+        constexpr int j = decltype(JJ)::value;
+        if constexpr (lat_owner<NB, VAR>(bb, j) == W) {
+          row_v_2l(E, C[bb][j]);
+          static_for<0, 4>([&](auto R) { C[bb][j][decltype(R)::value] *= rsr[decltype(R)::value]; });
+          lds_put(S.Uf[buf][j], C[bb][j], lane);
+          if constexpr (j == bb + 1) lat_signal(&S.unext[bb], 1, lane);
+        }
+      });
+      lat_signal(&S.ucount[bb], nown, lane);
+    }
+    constexpr bool look = lat_owner<NB, VAR>(bb + 1, bb + 1) == W;
+    constexpr bool trail = lat_any_trail<NB, VAR>(W, bb);
+    constexpr bool own_next = lat_owner<NB, VAR>(bb, bb + 1) == W;
+    auto ublk = [&](auto II) -> v4d {
+      constexpr int i = decltype(II)::value;
+      if constexpr (lat_owner<NB, VAR>(bb, i) == W) return C[bb][i];
+      else return lds_get(S.Uf[buf][i], lane);
+    };
+    if constexpr (look) {
+      if constexpr (!own_next) lat_wait(&S.unext[bb], 1, stall);
+      const v4d u = ublk(std::integral_constant<int, bb + 1>{});
+      syrk_update(C[bb + 1][bb + 1], u, u);
+      factor(std::integral_constant<int, bb + 1>{});
+    }
+    if constexpr (trail) lat_wait(&S.ucount[bb], NB - 1 - bb, stall);
+    static_for<bb + 1, NB>([&](auto II) {
+      constexpr int i = decltype(II)::value;
+      if constexpr (lat_trail_owned<NB, VAR>(W, bb, i)) {
+        const v4d ui = ublk(II);
+        static_for<i, NB>([&](auto JJ) {
+          constexpr int j = decltype(JJ)::value;
+          if constexpr (lat_owner<NB, VAR>(i, j) == W && !(i == bb + 1 && j == bb + 1)) {
+            if constexpr (j == i) syrk_update(C[i][j], ui, ui);
+            else syrk_update(C[i][j], ui, ublk(JJ));
+          }
+        });
+      }
+    });
+    lat_signal(&S.done[bb], 1, lane);
+  });
 }
 
 template <int NB, int W, bool STAMP, int VAR>
@@ -137,7 +269,16 @@ __device__ __forceinline__ void lat_wave(LatLds<NB>& S, const CholJob& J, const 
       }
     });
   });
-  constexpr bool PRE = VAR == LAT_VAR_DEFAULT;
+  constexpr bool PRE = lat_pre(VAR);
+  if constexpr (VAR == LAT_VAR_FLOW) {   // (visible to every wave after the prologue's barriers)
+    if (tid < NB) {
+      S.eflag[tid] = 0;
+      S.ucount[tid] = 0;
+      S.unext[tid] = 0;
+      S.done[tid] = 0;
+    }
+    if (tid == 0) S.stall = 0;
+  }
   static_assert(LD <= 256 && 2 * 256 >= STAGE_THETA_MAX, "one column / record per thread; theta row in two loads");
   if (PRE && J.urec != nullptr && ldth <= STAGE_THETA_MAX) {
     // the theta row arrived in tv (read at kernel entry); this thread's
@@ -254,13 +395,17 @@ __device__ __forceinline__ void lat_wave(LatLds<NB>& S, const CholJob& J, const 
     constexpr int bb = decltype(BBc)::value;
     diag_factor_2l<NB, bb, true, true>(C[bb][bb], E, rsr, q, c, ldet, ok, klast);
     if constexpr (bb < NB - 1) {
-      lds_put(S.E, E, lane);
-      static_for<0, 4>([&](auto R) { S.R[decltype(R)::value][lane] = rsr[decltype(R)::value]; });
+      lds_put(S.Ef[0], E, lane);
+      static_for<0, 4>([&](auto R) { S.Rf[0][decltype(R)::value][lane] = rsr[decltype(R)::value]; });
     } else {
       const double qv = readlane_d(C[bb][bb][3], 63);
       if (lane == 0) S.qv = qv;
     }
   };
+  if constexpr (VAR == LAT_VAR_FLOW) {
+    lat_flow<NB, W, STAMP, VAR>(S, C, E, rsr, q, c, lane, ldet, ok, klast);
+    return;
+  } else {
   if constexpr (lat_owner<NB, VAR>(0, 0) == W) factor(std::integral_constant<int, 0>{});
   static_for<0, NB - 1>([&](auto BBc) {
     constexpr int bb = decltype(BBc)::value;
@@ -269,8 +414,8 @@ __device__ __forceinline__ void lat_wave(LatLds<NB>& S, const CholJob& J, const 
     constexpr bool row_owned = lat_row_owned<NB, VAR>(W, bb);
     if constexpr (row_owned) {
       if constexpr (lat_owner<NB, VAR>(bb, bb) != W) {
-        E = lds_get(S.E, lane);
-        static_for<0, 4>([&](auto R) { rsr[decltype(R)::value] = S.R[decltype(R)::value][lane]; });
+        E = lds_get(S.Ef[0], lane);
+        static_for<0, 4>([&](auto R) { rsr[decltype(R)::value] = S.Rf[0][decltype(R)::value][lane]; });
       }
       static_for<bb + 1, NB>([&](auto JJ) {
         constexpr int j = decltype(JJ)::value;
@@ -280,7 +425,7 @@ __device__ __forceinline__ void lat_wave(LatLds<NB>& S, const CholJob& J, const 
         constexpr int j = decltype(JJ)::value;
         if constexpr (lat_owner<NB, VAR>(bb, j) == W) {
           static_for<0, 4>([&](auto R) { C[bb][j][decltype(R)::value] *= rsr[decltype(R)::value]; });
-          lds_put(S.U[j], C[bb][j], lane);
+          lds_put(S.Uf[0][j], C[bb][j], lane);
         }
       });
     }
@@ -288,7 +433,7 @@ __device__ __forceinline__ void lat_wave(LatLds<NB>& S, const CholJob& J, const 
     auto ublk = [&](auto II) -> v4d {
       constexpr int i = decltype(II)::value;
       if constexpr (lat_owner<NB, VAR>(bb, i) == W) return C[bb][i];
-      else return lds_get(S.U[i], lane);
+      else return lds_get(S.Uf[0][i], lane);
     };
     // lookahead: the next diagonal block first, then its panel
     if constexpr (lat_owner<NB, VAR>(bb + 1, bb + 1) == W) {
@@ -311,6 +456,7 @@ __device__ __forceinline__ void lat_wave(LatLds<NB>& S, const CholJob& J, const 
       }
     });
   });
+  }
   LAT_STAMP(10)
 }
 
@@ -328,7 +474,7 @@ __global__ __launch_bounds__(256) void chol_lat_kernel(const CholJob* __restrict
   // record and block loads (the round-3 prologue read the compact entries
   // after the record's index list had arrived: two latencies in series)
   double tv[2] = {0.0, 0.0};
-  if constexpr (VAR == LAT_VAR_DEFAULT) {
+  if constexpr (lat_pre(VAR)) {
     const double* t0 = theta + (long long)b * ldth;
     if (ldth <= STAGE_THETA_MAX) {
       if (tid < ldth) tv[0] = t0[tid];
@@ -357,6 +503,9 @@ __global__ __launch_bounds__(256) void chol_lat_kernel(const CholJob* __restrict
   if (tid == 0) {
     double lnl = J.K[(long long)b * J.kstride] - 0.5 * S.qv - 0.5 * (((S.ldet[0] + S.ldet[1]) + S.ldet[2]) + S.ldet[3]);
     if (!(S.ok[0] && S.ok[1] && S.ok[2] && S.ok[3]) || J.fail) lnl = -INFINITY;
+    if constexpr (VAR == LAT_VAR_FLOW) {
+      if (S.stall) lnl = NAN;
+    }
     out_units[(long long)p * B + b] = lnl;
     host_units[(long long)p * B + b] = lnl;    // pinned: the host folds the P terms after the launch
   }
@@ -387,14 +536,14 @@ int launch_chol_lat_t(int nb, const CholJob* jobs, int B, int P, const double* t
 int launch_chol_lat(int nb, const CholJob* jobs, int B, int P, const double* theta, int ldth, double* units,
                     double* host_units, hipStream_t st, bool stamp, int var) {
 #ifdef EWH_DEV
-  if (stamp) return launch_chol_lat_t<true, LAT_VAR_DEFAULT>(nb, jobs, B, P, theta, ldth, units, host_units, st);
-  if (var == LAT_VAR_MAP_ONLY)
-    return launch_chol_lat_t<false, LAT_VAR_MAP_ONLY>(nb, jobs, B, P, theta, ldth, units, host_units, st);
+  if (stamp) return launch_chol_lat_t<true, LAT_VAR_FLOW>(nb, jobs, B, P, theta, ldth, units, host_units, st);
+  if (var == LAT_VAR_BARRIER)
+    return launch_chol_lat_t<false, LAT_VAR_BARRIER>(nb, jobs, B, P, theta, ldth, units, host_units, st);
   if (var == LAT_VAR_R3) return launch_chol_lat_t<false, LAT_VAR_R3>(nb, jobs, B, P, theta, ldth, units, host_units, st);
 #endif
   (void)stamp;
   (void)var;
-  return launch_chol_lat_t<false, LAT_VAR_DEFAULT>(nb, jobs, B, P, theta, ldth, units, host_units, st);
+  return launch_chol_lat_t<false, LAT_VAR_FLOW>(nb, jobs, B, P, theta, ldth, units, host_units, st);
 }
 
 #ifdef EWH_DEV

@@ -16,7 +16,7 @@ void launch_chol_mfma(const CholJob* jobs, int B, long long u0, long long n, int
 }  // namespace
 
 #ifdef EWH_DEV
-// (24, 25: latency-kernel variants, chol_lat.hip LAT_VAR_MAP_ONLY / LAT_VAR_R3)
+// (24, 25: latency-kernel variants, chol_lat.hip LAT_VAR_BARRIER / LAT_VAR_R3)
 bool variant_built(int mode) {
   return mode == 15 || mode == 16 || mode == 17 || mode == 19 || mode == 21 || mode == 22 || mode == 24 || mode == 25;
 }
