@@ -21,3 +21,18 @@ def test_chol_variants_vs_oracle():
                        text=True, timeout=600)
     print(r.stdout[-4000:], r.stderr[-2000:])
     assert r.returncode == 0
+
+
+@pytest.mark.parametrize("mode", [0, 24, 25])
+def test_latency_variants_vs_batched(mode):
+    """chol_lat_kernel variants (0: the dataflow default, 24: the same with
+    block barriers, 25: the round-3 kernel) against the batched path on the
+    latency-test goldens (scripts/lat_variant_check.py)."""
+    lib = os.path.join(ROOT, "enterprise_warp_amd", "libewarp_hip_dev.so")
+    if not os.path.exists(lib):
+        pytest.skip("dev library not built (make -C enterprise_warp_amd/csrc dev)")
+    env = dict(os.environ, EWARP_HIP_LIB=lib)
+    r = subprocess.run([sys.executable, os.path.join(ROOT, "scripts", "lat_variant_check.py"), "--mode", str(mode)],
+                       capture_output=True, text=True, timeout=600, env=env)
+    print(r.stdout[-4000:], r.stderr[-2000:])
+    assert r.returncode == 0
