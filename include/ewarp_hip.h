@@ -256,7 +256,8 @@ double ewh_unit_cost(const ewh_handle* h, int32_t pulsar);
  * block row by MFMA with L^-1 -- when the matrix fits registers; the LDS
  * kernel otherwise; batches of up to 8 samples on one device take the
  * latency kernel, one 4-wave workgroup per (pulsar, sample) with theta read
- * from pinned memory and the pulsar fold fused), 2 = the default without
+ * from pinned memory and the unit terms written to pinned memory, folded by
+ * the host), 2 = the default without
  * that latency path (batched kernels at every batch size), 1 = force the
  * LDS kernel (unblocked Cholesky; for a
  * correlated common process also the round-1 dense LDS diagonal-block and
@@ -269,7 +270,9 @@ double ewh_unit_cost(const ewh_handle* h, int32_t pulsar);
  * pipelined contraction with 4 / 8 waves per sample (default: 8 for 144+
  * columns, else 4), 17 = the round-2 one-level panel (NB = 8), 19 = the default with the spectra read through the CSR tables
  * instead of the staged records, 21 = the default with in-kernel phase
- * stamps (NB = 8, ewh_dev_stamps).  Other modes
+ * stamps (NB = 8, ewh_dev_stamps), 22 = the latency kernel with phase
+ * stamps (ewh_dev_lat_stamps), 24 / 25 = the latency kernel with block
+ * barriers instead of the dataflow panel loop / as in round 3.  Other modes
  * return EWH_E_UNSUPPORTED. */
 int ewh_set_kernel_mode(ewh_handle* h, int32_t mode);
 
