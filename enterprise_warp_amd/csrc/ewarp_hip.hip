@@ -2231,9 +2231,6 @@ struct ewh_handle {
   // latency path: device addresses of h_theta / h_out (for the host pointers recorded)
   const double *lat_th_host = nullptr, *lat_out_host = nullptr;
   double *lat_th_dev = nullptr, *lat_out_dev = nullptr;
-  // dev mode 27: theta staged in host-written fine-grained device memory
-  double* lat_th_fg = nullptr;
-  size_t lat_th_fg_cap = 0;
 };
 
 namespace {
@@ -2342,7 +2339,7 @@ int lnl_batch_single(ewh_handle* H, DevCtx* h, int B, double* out_host) {
   EWH_HIP(hipSetDevice(h->device));
   if ((rc = ensure_pinned(&H->h_out, &H->h_out_cap, (size_t)B))) return rc;
   const int km = h->kernel_mode;
-  if (h->lat_nb > 0 && B <= LAT_B_MAX && (km == 0 || km == 22 || km == 24 || km == 25 || km == 27)) {
+  if (h->lat_nb > 0 && B <= LAT_B_MAX && (km == 0 || km == 22 || km == 24 || km == 25)) {
     // latency path: one launch reads theta from the pinned staging and writes
     // the unit terms to pinned memory (chol_lat.hip); the host folds them
     if ((rc = ensure_units(h, B)) || (rc = ensure_pinned(&H->h_out, &H->h_out_cap, (size_t)h->P * B))) return rc;
@@ -2356,24 +2353,6 @@ int lnl_batch_single(ewh_handle* H, DevCtx* h, int B, double* out_host) {
       H->lat_out_host = H->h_out;
     }
     double *th_dev = H->lat_th_dev, *out_dev = H->lat_out_dev;
-#ifdef EWH_DEV
-    if (km == 27) {
-      // dev A/B: theta in fine-grained device memory the host stores to
-      // through the BAR (the kernel then reads it from HBM, not over PCIe)
-      const size_t need = (size_t)B * std::max(1, h->n_param);
-      if (need > H->lat_th_fg_cap) {
-        if (H->lat_th_fg) (void)hipFree(H->lat_th_fg);
-        H->lat_th_fg = nullptr;
-        H->lat_th_fg_cap = 0;
-        EWH_HIP(hipExtMallocWithFlags((void**)&H->lat_th_fg, sizeof(double) * need, hipDeviceMallocFinegrained));
-        H->lat_th_fg_cap = need;
-      }
-      volatile double* dst = H->lat_th_fg;
-      for (size_t i = 0; i < need; ++i) dst[i] = H->h_theta[i];
-      std::atomic_thread_fence(std::memory_order_seq_cst);
-      th_dev = H->lat_th_fg;
-    }
-#endif
     // every unit term lands in pinned memory; the host waits for them by
     // spinning on a sentinel (a NaN payload the kernel never writes: its
     // terms are finite or -inf) instead of a stream synchronisation, whose
@@ -2525,8 +2504,7 @@ int ewh_set_fixed_white(ewh_handle* H, const double* values) {
 
 int ewh_set_kernel_mode(ewh_handle* H, int32_t mode) {
   if (!H || mode < 0 || mode > 30) return set_err(EWH_E_INVALID, "bad handle / mode");
-  // (27: the latency path with theta in host-written fine-grained device memory, dev library)
-  if (mode != 0 && mode != 1 && mode != 2 && mode != 7 && !variant_built(mode) && !(mode == 27 && variant_built(24)))
+  if (mode != 0 && mode != 1 && mode != 2 && mode != 7 && !variant_built(mode))
     return set_err(EWH_E_UNSUPPORTED, "kernel mode " + std::to_string(mode) +
                                           " is not built into this library (A/B variants: the dev library, make dev)");
   for (DevCtx* h : H->ctx) {
@@ -2753,7 +2731,6 @@ void ewh_destroy(ewh_handle* H) {
   for (DevCtx* c : H->ctx) destroy_ctx(c);
   if (H->h_theta) (void)hipHostFree(H->h_theta);
   if (H->h_out) (void)hipHostFree(H->h_out);
-  if (H->lat_th_fg) (void)hipFree(H->lat_th_fg);
   delete H;
 }
 
