@@ -55,8 +55,12 @@ constexpr unsigned char LAT_MAP[9][8][8] = {{},
 // panel loop as a dataflow over LDS counters (lat_flow); dev A/B only:
 // LAT_VAR_BARRIER -- the same with two block barriers per panel;
 // LAT_VAR_R3 -- the round-3 kernel ((i + j) mod 4, theta after the job record).
-[[maybe_unused]] constexpr int LAT_VAR_FLOW = 0, LAT_VAR_BARRIER = 1, LAT_VAR_R3 = 2;
+// LAT_VAR_STALL (dev test only): LAT_VAR_FLOW with every wait running out at
+// once, so the stall path (LAT_STALL_BITS -> an error of ewh_lnl_batch) is
+// exercised (tests/test_gpu_properties.py).
+[[maybe_unused]] constexpr int LAT_VAR_FLOW = 0, LAT_VAR_BARRIER = 1, LAT_VAR_R3 = 2, LAT_VAR_STALL = 3;
 constexpr bool lat_pre(int var) { return var != LAT_VAR_R3; }
+constexpr bool lat_is_flow(int var) { return var == LAT_VAR_FLOW || var == LAT_VAR_STALL; }
 template <int NB, int VAR>
 constexpr int lat_owner(int i, int j) { return VAR == LAT_VAR_R3 ? (i + j) & 3 : LAT_MAP[NB][i][j]; }
 // wave w owns a block (bb, j > bb) of block row bb
@@ -125,21 +129,24 @@ struct LatLds {
   int ucount[NB];           // U blocks of block row k published
   int unext[NB];            // 1: U block (k, k + 1) published (the lookahead's operand)
   int done[NB];             // waves through panel k
-  int stall;                // a wait ran out (never expected): the unit term becomes NaN
+  int stall;                // a wait ran out (never expected): the unit term becomes LAT_STALL_BITS
 };
 
 // LAT_VAR_FLOW synchronisation through LDS counters: a wave publishes with
 // one workgroup-scope release add by lane 0 (after the wave's own LDS
 // writes), a consumer spins with acquire loads.  Every wait targets data
 // produced earlier in some wave's program order (the panel dependency DAG),
-// and is bounded: a wait that runs out marks the unit (NaN term) and goes on.
+// and is bounded: a wait that runs out marks the unit and goes on; the unit's
+// term is then the NaN payload LAT_STALL_BITS (ewarp_dev.h), which the host
+// turns into an error of ewh_lnl_batch (never a NaN lnL).
 constexpr int LAT_SPIN_MAX = 1 << 22;
 __device__ __forceinline__ void lat_signal(int* f, int add, int lane) {
   if (lane == 0) __hip_atomic_fetch_add(f, add, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_WORKGROUP);
 }
+template <bool FORCE = false>
 __device__ __forceinline__ void lat_wait(int* f, int target, int* stall) {
   for (int n = 0; __hip_atomic_load(f, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_WORKGROUP) < target; ++n) {
-    if (n >= LAT_SPIN_MAX) {
+    if (FORCE || n >= LAT_SPIN_MAX) {
       *stall = 1;
       break;
     }
@@ -175,7 +182,7 @@ __device__ __forceinline__ void lat_flow(LatLds<NB>& S, v4d (&C)[NB][NB], v4d& E
     constexpr int bb = decltype(BBc)::value;
     diag_factor_2l<NB, bb, true, true>(C[bb][bb], E, rsr, q, c, ldet, ok, klast);
     if constexpr (bb < NB - 1) {
-      if constexpr (bb >= LAT_NBUF) lat_wait(&S.done[bb - LAT_NBUF], 4, stall);
+      if constexpr (bb >= LAT_NBUF) lat_wait<VAR == LAT_VAR_STALL>(&S.done[bb - LAT_NBUF], 4, stall);
       lds_put(S.Ef[bb % LAT_NBUF], E, lane);
       static_for<0, 4>([&](auto R) { S.Rf[bb % LAT_NBUF][decltype(R)::value][lane] = rsr[decltype(R)::value]; });
       lat_signal(&S.eflag[bb], 1, lane);
@@ -191,12 +198,12 @@ __device__ __forceinline__ void lat_flow(LatLds<NB>& S, v4d (&C)[NB][NB], v4d& E
     constexpr int nown = lat_row_count<NB, VAR>(W, bb);
     if constexpr (nown > 0) {
       if constexpr (lat_owner<NB, VAR>(bb, bb) != W) {
-        lat_wait(&S.eflag[bb], 1, stall);
+        lat_wait<VAR == LAT_VAR_STALL>(&S.eflag[bb], 1, stall);
         E = lds_get(S.Ef[buf], lane);
         static_for<0, 4>([&](auto R) { rsr[decltype(R)::value] = S.Rf[buf][decltype(R)::value][lane]; });
       }
       LAT_STAMP(3 + bb)
-      if constexpr (bb >= LAT_NBUF) lat_wait(&S.done[bb - LAT_NBUF], 4, stall);
+      if constexpr (bb >= LAT_NBUF) lat_wait<VAR == LAT_VAR_STALL>(&S.done[bb - LAT_NBUF], 4, stall);
       // block by block, (bb, bb + 1) first: the next diagonal block's owner
       // waits on that one alone
       static_for<bb + 1, NB>([&](auto JJ) {
@@ -219,12 +226,12 @@ __device__ __forceinline__ void lat_flow(LatLds<NB>& S, v4d (&C)[NB][NB], v4d& E
       else return lds_get(S.Uf[buf][i], lane);
     };
     if constexpr (look) {
-      if constexpr (!own_next) lat_wait(&S.unext[bb], 1, stall);
+      if constexpr (!own_next) lat_wait<VAR == LAT_VAR_STALL>(&S.unext[bb], 1, stall);
       const v4d u = ublk(std::integral_constant<int, bb + 1>{});
       syrk_update(C[bb + 1][bb + 1], u, u);
       factor(std::integral_constant<int, bb + 1>{});
     }
-    if constexpr (trail) lat_wait(&S.ucount[bb], NB - 1 - bb, stall);
+    if constexpr (trail) lat_wait<VAR == LAT_VAR_STALL>(&S.ucount[bb], NB - 1 - bb, stall);
     static_for<bb + 1, NB>([&](auto II) {
       constexpr int i = decltype(II)::value;
       if constexpr (lat_trail_owned<NB, VAR>(W, bb, i)) {
@@ -271,7 +278,7 @@ __device__ __forceinline__ void lat_wave(LatLds<NB>& S, const CholJob& J, const 
     });
   });
   constexpr bool PRE = lat_pre(VAR);
-  if constexpr (VAR == LAT_VAR_FLOW) {   // (visible to every wave after the prologue's barriers)
+  if constexpr (lat_is_flow(VAR)) {   // (visible to every wave after the prologue's barriers)
     if (tid < NB) {
       S.eflag[tid] = 0;
       S.ucount[tid] = 0;
@@ -403,7 +410,7 @@ __device__ __forceinline__ void lat_wave(LatLds<NB>& S, const CholJob& J, const 
       if (lane == 0) S.qv = qv;
     }
   };
-  if constexpr (VAR == LAT_VAR_FLOW) {
+  if constexpr (lat_is_flow(VAR)) {
     lat_flow<NB, W, STAMP, VAR>(S, C, E, rsr, q, c, lane, ldet, ok, klast);
     return;
   } else {
@@ -504,8 +511,8 @@ __global__ __launch_bounds__(256) void chol_lat_kernel(const CholJob* __restrict
   if (tid == 0) {
     double lnl = J.K[(long long)b * J.kstride] - 0.5 * S.qv - 0.5 * (((S.ldet[0] + S.ldet[1]) + S.ldet[2]) + S.ldet[3]);
     if (!(S.ok[0] && S.ok[1] && S.ok[2] && S.ok[3]) || J.fail) lnl = -INFINITY;
-    if constexpr (VAR == LAT_VAR_FLOW) {
-      if (S.stall) lnl = NAN;
+    if constexpr (lat_is_flow(VAR)) {
+      if (S.stall) lnl = __builtin_bit_cast(double, LAT_STALL_BITS);
     }
     out_units[(long long)p * B + b] = lnl;
     host_units[(long long)p * B + b] = lnl;    // pinned: the host folds the P terms after the launch
@@ -541,6 +548,8 @@ int launch_chol_lat(int nb, const CholJob* jobs, int B, int P, const double* the
   if (var == LAT_VAR_BARRIER)
     return launch_chol_lat_t<false, LAT_VAR_BARRIER>(nb, jobs, B, P, theta, ldth, units, host_units, st);
   if (var == LAT_VAR_R3) return launch_chol_lat_t<false, LAT_VAR_R3>(nb, jobs, B, P, theta, ldth, units, host_units, st);
+  if (var == LAT_VAR_STALL)
+    return launch_chol_lat_t<false, LAT_VAR_STALL>(nb, jobs, B, P, theta, ldth, units, host_units, st);
 #endif
   (void)stamp;
   (void)var;

@@ -6,19 +6,22 @@
 namespace ewh_dev {
 namespace {
 
-template <int NB, int ALG = PANEL_2L, bool STAMP = false>
+template <int NB, int ALG = PANEL_2L, bool STAMP = false, int W = default_waves(NB), bool FULL = false>
 void launch_chol_mfma(const CholJob* jobs, int B, long long u0, long long n, int b_off, const double* theta, int ldth,
                       double* units, hipStream_t st) {
-  hipLaunchKernelGGL(HIP_KERNEL_NAME(chol_mfma_kernel<NB, default_waves(NB), ALG, STAMP, 0>), dim3((unsigned)n),
+  hipLaunchKernelGGL(HIP_KERNEL_NAME(chol_mfma_kernel<NB, W, ALG, STAMP, 0, FULL>), dim3((unsigned)n),
                      dim3(64), 0, st, jobs, B, u0, b_off, theta, ldth, units, nullptr, 0, 0);
 }
 
 }  // namespace
 
 #ifdef EWH_DEV
-// (24, 25: latency-kernel variants, chol_lat.hip LAT_VAR_BARRIER / LAT_VAR_R3)
+// (23: the latency kernel with every wait forced to run out, LAT_VAR_STALL;
+// 24, 25: latency-kernel variants, chol_lat.hip LAT_VAR_BARRIER / LAT_VAR_R3;
+// 26: one wave per SIMD, whole triangle resident, plain right-looking order)
 bool variant_built(int mode) {
-  return mode == 15 || mode == 16 || mode == 17 || mode == 19 || mode == 21 || mode == 22 || mode == 24 || mode == 25;
+  return mode == 15 || mode == 16 || mode == 17 || mode == 19 || mode == 21 || mode == 22 || mode == 23 ||
+         mode == 24 || mode == 25 || mode == 26;
 }
 // phase stamps of kernel mode 21 (g_stamps: STAMP_UNITS x STAMP_N)
 extern "C" int ewh_dev_stamps(long long* out, long long n) {
@@ -37,6 +40,7 @@ int launch_chol_small(int mode, int nb, const CholJob* jobs, int B, long long u0
     switch (mode) {
       case 17: launch_chol_mfma<8, PANEL_1L>(jobs, B, u0, n, b_off, theta, ldth, units, st); return 0;  // round-2 one-level panel
       case 21: launch_chol_mfma<8, PANEL_2L, true>(jobs, B, u0, n, b_off, theta, ldth, units, st); return 0;  // default + phase stamps
+      case 26: launch_chol_mfma<8, PANEL_2L, false, 1, true>(jobs, B, u0, n, b_off, theta, ldth, units, st); return 0;  // W = 1, FULL
       default: break;
     }
   }

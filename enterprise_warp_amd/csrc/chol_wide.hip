@@ -1,0 +1,178 @@
+// chol_wide.hip — the factorisation at any width: bases wider than the
+// register kernels take (reduced width > 16 blocks = 255 columns, e.g.
+// red_general_freqs / X_<n>_nfreqs models, enterprise_models.py:148-167,
+// :436-468), and the partial factorisation of a correlated common process
+// wider than chol_mfma_kernel<..., KEEP> takes (> 9 blocks).
+//
+// One wave per (pulsar, sample), left-looking over block rows (as
+// chol_big_kernel), with NB a runtime value: block row i is processed in
+// chunks of CW 16x16 blocks held in registers in the MFMA C/D layout; each
+// chunk takes the updates A_ij -= U_pi^T U_pj of every finished row p < i
+// (four f64 MFMAs per block, U streamed back from a per-workgroup scratch),
+// then -- chunk 0 holds the diagonal block -- the two-level LDL^T panel of
+// the batched kernels (diag_factor_2l; E = L^-T and the row scales are kept
+// in registers for the row's later chunks), V = E^T A and U = D^-1/2 V
+// (row_v_2l), and is written back to the scratch.  Per block the same
+// operations in the same order as chol_big_kernel / chol_mfma_kernel.
+//
+// keep > 0: only block rows 0..NB-keep-1 are factored; the trailing keep x
+// keep blocks (the common columns + r of a correlated process) take the
+// updates of every factored row and are written to keep_out as a dense
+// (16 keep)^2 square, pulsar-major -- the layout of chol_mfma_kernel<KEEP>.
+#include "ewarp_dev.h"
+
+namespace ewh_dev {
+namespace {
+
+constexpr int CW = 8;                // blocks of a block row per register chunk
+typedef __attribute__((address_space(1))) v4d gv4d;
+
+__device__ __forceinline__ long long wide_blk(int p, int j, int nb) {   // packed upper block index
+  return (long long)p * nb - (long long)p * (p - 1) / 2 + (j - p);
+}
+
+__global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(2, 2)))
+void chol_wide_kernel(const CholJob* __restrict__ jobs, int B, long long u0, int b_off,
+                      const double* __restrict__ theta, int ldth, double* __restrict__ out_units,
+                      double* __restrict__ scratch, long long scr_per_wg, int keep, double* __restrict__ keep_out,
+                      int keep_b0, int keep_bs) {
+  __shared__ double phinv[WIDE_LD_MAX];
+  const int lane = threadIdx.x, q = lane >> 4, c = lane & 15;
+  const long long u = u0 + xcd_unit(blockIdx.x, gridDim.x);
+  const int p = (int)(u / B), b = (int)(u % B);
+  const CholJob J = jobs[p];
+  const int LD = J.ld, NB = LD >> 4;
+  const int nfact = NB - keep;
+  const gdptr A = (gdptr)(J.mats + (long long)(b - b_off) * J.mstride);
+  const double* th = theta + (long long)b * ldth;
+  __attribute__((address_space(1))) double* scr =
+      (__attribute__((address_space(1))) double*)(scratch + (long long)blockIdx.x * scr_per_wg + lane * 4);
+
+  LogAcc lphi;
+  for (int a = lane; a < LD; a += 64) {
+    double pi = 0.0;
+    if (a < J.mreal && J.col_ptr[a] < J.col_ptr[a + 1]) {   // (pads carry no entry)
+      double ph = 0.0;
+      for (int e = J.col_ptr[a]; e < J.col_ptr[a + 1]; ++e) ph += spec_phi_body(J.spec[e], th);
+      pi = 1.0 / ph;
+      lphi.add(ph);
+    }
+    phinv[a] = pi;
+  }
+  const double lphi_sum = wave_sum(lphi.value());
+  __syncthreads();
+
+  LogAcc ldet;
+  bool ok = true;
+  double qv = 0.0;
+  const int klast = __builtin_amdgcn_readfirstlane(J.mreal - 16 * (NB - 1));
+  const int KD = 16 * keep;
+  double* ko = keep > 0 ? keep_out + ((long long)p * keep_bs + (b - keep_b0)) * ((long long)KD * KD) : nullptr;
+#pragma unroll 1
+  for (int i = 0; i < NB; ++i) {
+    const bool fact = i < nfact;
+    const bool lastr = keep == 0 && i == NB - 1;         // the block row holding the residual
+    const int pmax = min(i, nfact);
+    v4d E = {0.0, 0.0, 0.0, 0.0};
+    double rsr[4] = {1.0, 1.0, 1.0, 1.0};
+#pragma unroll 1
+    for (int c0 = i; c0 < NB; c0 += CW) {
+      v4d R[CW];
+      static_for<0, CW>([&](auto JJ) {
+        constexpr int jj = decltype(JJ)::value;
+        const int j = c0 + jj;
+        if (j < NB) {
+          static_for<0, 4>([&](auto RR) {
+            constexpr int r = decltype(RR)::value;
+            R[jj][r] = A[(long long)(16 * i + q + 4 * r) * LD + 16 * j + c];
+          });
+          if (j == i) {
+            const double pd = phinv[16 * i + c];
+            static_for<0, 4>([&](auto RR) {
+              constexpr int r = decltype(RR)::value;
+              R[jj][r] += (q + 4 * r == c) ? pd : 0.0;
+            });
+          }
+        } else {
+          R[jj] = v4d{0.0, 0.0, 0.0, 0.0};
+        }
+      });
+#pragma unroll 1
+      for (int pp = 0; pp < pmax; ++pp) {
+        const v4d Ui = *(const gv4d*)(scr + wide_blk(pp, i, NB) * 256);
+        static_for<0, CW>([&](auto JJ) {
+          constexpr int jj = decltype(JJ)::value;
+          if (c0 + jj < NB) {
+            const v4d Uj = *(const gv4d*)(scr + wide_blk(pp, c0 + jj, NB) * 256);
+            syrk_update(R[jj], Ui, Uj);
+          }
+        });
+      }
+      if (fact) {
+        if (c0 == i) {
+          // (template arguments pick the panel form: <1, 0, true> is the
+          // residual block row, <2, 0, true> an ordinary one)
+          if (lastr) {
+            diag_factor_2l<1, 0, true>(R[0], E, rsr, q, c, ldet, ok, klast);
+            qv = readlane_d(R[0][3], 63);
+          } else {
+            diag_factor_2l<2, 0, true>(R[0], E, rsr, q, c, ldet, ok, 16);
+          }
+        }
+        static_for<0, CW>([&](auto JJ) {
+          constexpr int jj = decltype(JJ)::value;
+          const int j = c0 + jj;
+          if (j > i && j < NB) {
+            row_v_2l(E, R[jj]);
+            static_for<0, 4>([&](auto RR) { R[jj][decltype(RR)::value] *= rsr[decltype(RR)::value]; });
+            *(gv4d*)(scr + wide_blk(i, j, NB) * 256) = R[jj];
+          }
+        });
+      } else {
+        // a kept block row: the updated blocks (i, j >= i) to the dense square
+        static_for<0, CW>([&](auto JJ) {
+          constexpr int jj = decltype(JJ)::value;
+          const int j = c0 + jj;
+          if (j < NB) {
+            static_for<0, 4>([&](auto RR) {
+              constexpr int r = decltype(RR)::value;
+              const int row = 16 * (i - nfact) + q + 4 * r, col = 16 * (j - nfact) + c;
+              if (i != j || row <= col) {
+                ko[(long long)row * KD + col] = R[jj][r];
+                ko[(long long)col * KD + row] = R[jj][r];
+              }
+            });
+          }
+        });
+      }
+    }
+  }
+  const double ldet_v = wave_sum(ldet.value());
+  const bool ok_all = __all(ok);
+  if (lane == 0) {
+    double lnl = J.K[(long long)(b - b_off) * J.kstride] - 0.5 * qv - 0.5 * ldet_v - 0.5 * lphi_sum;
+    if (!ok_all || J.fail) lnl = -INFINITY;
+    out_units[(long long)p * B + b] = lnl;
+  }
+}
+
+}  // namespace
+
+long long wide_scratch_per_wg(int nb, int keep) {
+  const int nf = nb - keep;
+  long long n = 0;
+  for (int p = 0; p < nf; ++p) n += nb - p;
+  return n * 256;
+}
+
+int launch_chol_wide(const CholJob* jobs, int B, long long u0, long long n, int b_off, const double* theta, int ldth,
+                     double* units, double* scr, long long scr_per_wg, long long cap, int keep, double* keep_out,
+                     int keep_b0, int keep_bs, hipStream_t st) {
+  for (long long o = 0; o < n; o += cap)   // one scratch slot per workgroup of a launch
+    hipLaunchKernelGGL(chol_wide_kernel, dim3((unsigned)std::min(cap, n - o)), dim3(64), 0, st, jobs, B, u0 + o, b_off,
+                       theta, ldth, units, scr, scr_per_wg, keep, keep_out, keep_b0, keep_bs);
+  const hipError_t e = hipGetLastError();
+  return e == hipSuccess ? 0 : set_err(EWH_E_HIP, std::string("chol_wide_kernel: ") + hipGetErrorString(e));
+}
+
+}  // namespace ewh_dev

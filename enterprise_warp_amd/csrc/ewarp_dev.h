@@ -191,9 +191,44 @@ static __device__ double block_sum256(double v, double* scratch) {
 }
 
 // ----------------------------------------------------------------------------
+// double-double helpers (Knuth TwoSum, TwoProd by fma; Dekker / Bailey
+// normalisation): value = hi + lo with |lo| <= ulp(hi) / 2
+// ----------------------------------------------------------------------------
+struct dd {
+  double hi, lo;
+};
+__device__ __forceinline__ dd dd_two_sum(double a, double b) {
+  const double s = a + b, bp = s - a;
+  return {s, (a - (s - bp)) + (b - bp)};
+}
+__device__ __forceinline__ dd dd_fast(double a, double b) {   // |a| >= |b|
+  const double s = a + b;
+  return {s, b - (s - a)};
+}
+__device__ __forceinline__ dd dd_add(dd x, dd y) {
+  const dd s = dd_two_sum(x.hi, y.hi);
+  return dd_fast(s.hi, s.lo + x.lo + y.lo);
+}
+__device__ __forceinline__ dd dd_mul(dd x, dd y) {
+  const double p = x.hi * y.hi;
+  return dd_fast(p, fma(x.hi, y.hi, -p) + (x.hi * y.lo + x.lo * y.hi));
+}
+__device__ __forceinline__ dd dd_div(dd x, dd y) {          // one Newton correction of x.hi / y.hi
+  const double q = x.hi / y.hi;
+  const dd r = dd_add(x, dd_mul({-q, 0.0}, y));
+  return dd_fast(q, r.hi / y.hi);
+}
+__device__ __forceinline__ dd dd_sqrt(dd x) {
+  const double r = sqrt(x.hi);
+  const dd e = dd_add(x, dd_mul({-r, 0.0}, {r, 0.0}));
+  return dd_fast(r, e.hi / (2.0 * r));
+}
+
+// ----------------------------------------------------------------------------
 // per-pulsar device tables
 // ----------------------------------------------------------------------------
 constexpr int CT_ROWS = 32;   // TOA rows per contraction tile (8 MFMA k-steps); T_aug is padded by this many zero rows
+constexpr int CT_GROUP = 2;   // contract2: tiles per compensated-accumulation group (a power of two)
 
 struct PsrDev {
   int n_toa, m, ld, nb;      // varying layout: T_aug is n_toa x ld, r at ld-1
@@ -241,6 +276,9 @@ struct CholJob {
   // indices are positions in this list); 0: the whole theta row is staged
   int ntidx = 0;
   int tidx[16] = {};
+  // the low part of a double-double matrix (chol_dd_kernel; same stride as
+  // mats), or NULL
+  const double* mats_lo = nullptr;
 };
 
 // one distinct spectrum of a fixed-WN job: phi = sum of its ne entries
@@ -390,14 +428,18 @@ constexpr bool wave_uses(int nb, int wave, int j, int W = 4) {
   return false;
 }
 
-template <int NB, int WAVE, int W>
+// WAVE / W: the physical wave and waves per workgroup (tile copies, the
+// per-tile weights); VW / WS: the virtual wave that picks the output blocks
+// (blocks VW + WS sl) and the virtual waves per sample -- WS = W SPLIT when a
+// sample's blocks are split over SPLIT workgroups (contract2_kernel).
+template <int NB, int WAVE, int W, int VW = WAVE, int WS = W>
 __device__ __forceinline__ void contract2_body(const PsrDev& P, const double* __restrict__ wrow,
                                                const double* __restrict__ brow, double* __restrict__ srow,
                                                double* __restrict__ Gout) {
   extern __shared__ __attribute__((aligned(16))) double smem[];
   constexpr int LD = 16 * NB;
   constexpr int NBLK = NB * (NB + 1) / 2;
-  constexpr int SLOTS = (NBLK - WAVE + W - 1) / W;
+  constexpr int SLOTS = (NBLK - VW + WS - 1) / WS;
   constexpr int TILE = CT_ROWS * LD;                 // doubles per tile
   constexpr int CHUNKS = TILE * 8 / 1024;            // 1-KiB glds pieces per tile (4 NB), dealt round-robin to the W waves
   static_assert(CHUNKS * 1024 == TILE * 8, "tile must split into pieces of 1 KiB");
@@ -409,9 +451,34 @@ __device__ __forceinline__ void contract2_body(const PsrDev& P, const double* __
   int* const ebase = (int*)(ewbase + 2 * CT_ROWS);
   int* const fmbase = ebase + 2 * CT_ROWS;
 
-  v4d acc[SLOTS > 0 ? SLOTS : 1];
+  // compensated accumulation: each group of CT_GROUP tiles
+  // (CT_GROUP x 32 TOA rows) is summed by the MFMAs into a fresh accumulator
+  // acc, which is then added into the running sum hi + lo by TwoSum (Knuth:
+  // exact); G = hi + lo at the end.  A single fp64 accumulator over all rows
+  // lost up to ~30x the strict bound of lnL on ill-conditioned prior draws
+  // through the timing-model / red-noise near-degeneracy (tests/golden
+  // c4_small sample 0: 4.0 vs enterprise's 2.3 strict); per group the error
+  // grows only over CT_GROUP x 32 rows.
+  v4d acc[SLOTS > 0 ? SLOTS : 1], hi[SLOTS > 0 ? SLOTS : 1], lo[SLOTS > 0 ? SLOTS : 1];
 #pragma unroll
-  for (int sl = 0; sl < SLOTS; ++sl) acc[sl] = v4d{0.0, 0.0, 0.0, 0.0};
+  for (int sl = 0; sl < SLOTS; ++sl) {
+    acc[sl] = v4d{0.0, 0.0, 0.0, 0.0};
+    hi[sl] = v4d{0.0, 0.0, 0.0, 0.0};
+    lo[sl] = v4d{0.0, 0.0, 0.0, 0.0};
+  }
+  auto flush = [&]() {
+    static_for<0, SLOTS>([&](auto SL) {
+      constexpr int sl = decltype(SL)::value;
+      static_for<0, 4>([&](auto R) {
+        constexpr int r = decltype(R)::value;
+        const double a = hi[sl][r], b = acc[sl][r];
+        const double sum = a + b, bp = sum - a;
+        lo[sl][r] += (a - (sum - bp)) + (b - bp);
+        hi[sl][r] = sum;
+        acc[sl][r] = 0.0;
+      });
+    });
+  };
 
   const bool ecorr = P.n_epoch > 0;
   double eacc = 0.0;                                 // running s_e of column `tid`
@@ -482,11 +549,11 @@ __device__ __forceinline__ void contract2_body(const PsrDev& P, const double* __
         double tv[NB], av[NB];
         static_for<0, NB>([&](auto J) {
           constexpr int j = decltype(J)::value;
-          if constexpr (wave_uses(NB, WAVE, j, W)) tv[j] = trow[16 * j];
-          if constexpr (wave_uses_row(NB, WAVE, j, W)) av[j] = wr * tv[j];
+          if constexpr (wave_uses(NB, VW, j, WS)) tv[j] = trow[16 * j];
+          if constexpr (wave_uses_row(NB, VW, j, WS)) av[j] = wr * tv[j];
         });
         static_for<0, SLOTS>([&](auto SL) {
-          constexpr int blk = WAVE + W * decltype(SL)::value;
+          constexpr int blk = VW + WS * decltype(SL)::value;
           constexpr int bi = tri_i(NB, blk), bj = tri_j(NB, blk);
           acc[decltype(SL)::value] = __builtin_amdgcn_mfma_f64_16x16x4f64(av[bi], tv[bj], acc[decltype(SL)::value], 0, 0, 0);
         });
@@ -523,6 +590,7 @@ __device__ __forceinline__ void contract2_body(const PsrDev& P, const double* __
           }
         }
       }
+      if ((it & (CT_GROUP - 1)) == CT_GROUP - 1 || it + 1 == ntile) flush();
       if (it + 1 < ntile) stage(cur ^ 1, it + 1);
       __syncthreads();                               // drains the glds of tile it+1 (vmcnt(0))
     }
@@ -539,12 +607,12 @@ __device__ __forceinline__ void contract2_body(const PsrDev& P, const double* __
   // epilogue: C/D layout lane -> (row q + 4r, col c); mirror to the lower half,
   // unit diagonal on pad columns (m .. LD-2) so they factor as identity.
   static_for<0, SLOTS>([&](auto SL) {
-    constexpr int blk = WAVE + W * decltype(SL)::value;
+    constexpr int blk = VW + WS * decltype(SL)::value;
     constexpr int bi = tri_i(NB, blk), bj = tri_j(NB, blk);
 #pragma unroll
     for (int r = 0; r < 4; ++r) {
       const int row = 16 * bi + q + 4 * r, col = 16 * bj + c;
-      double v = acc[decltype(SL)::value][r];
+      double v = hi[decltype(SL)::value][r] + lo[decltype(SL)::value][r];
       if (row == col && row >= P.m && row < LD - 1) v = 1.0;
       Gout[(long long)row * LD + col] = v;
       Gout[(long long)col * LD + row] = v;
@@ -552,23 +620,33 @@ __device__ __forceinline__ void contract2_body(const PsrDev& P, const double* __
   });
 }
 
-// W = 4 or 8 waves per sample (8: half the accumulators per wave, so the
-// narrow NB = 9 kernel fits 4 waves per SIMD and the wide NB = 13 one 2)
-template <int NB, int W>
+// W = 4 or 8 waves per workgroup (8: half the accumulators per wave, so the
+// narrow NB = 9 kernel fits 2 waves per SIMD).  SPLIT = 2 (wide bases,
+// contract2_split): a sample's output blocks are split over two workgroups
+// (blockIdx.y), each streaming the whole basis, so the three accumulator
+// sets of the compensated sum fit the register budget; each half has its own
+// epoch-sum scratch row (s_stride apart).
+template <int NB, int W, int SPLIT = 1>
 __global__ __launch_bounds__(64 * W) void contract2_kernel(PsrDev P, const double* __restrict__ w,
                                                            const double* __restrict__ beta, double* __restrict__ s,
                                                            long long s_stride, double* __restrict__ G) {
   constexpr int LD = 16 * NB;
-  const int bl = blockIdx.x;
+  const int bl = blockIdx.x, half = SPLIT > 1 ? (int)blockIdx.y : 0;
   const double* wrow = w + (long long)bl * P.n_toa;
   const double* brow = beta + (long long)bl * P.n_epoch;
-  double* srow = s + (long long)bl * s_stride;
+  double* srow = s + ((long long)bl * SPLIT + half) * s_stride;
   double* Gout = G + (long long)bl * LD * LD;
   const int wv = threadIdx.x >> 6;
-  static_for<0, W>([&](auto WV) {
-    if (wv == decltype(WV)::value) contract2_body<NB, decltype(WV)::value, W>(P, wrow, brow, srow, Gout);
+  static_for<0, SPLIT>([&](auto H) {
+    static_for<0, W>([&](auto WV) {
+      constexpr int h = decltype(H)::value, wave = decltype(WV)::value;
+      if (half == h && wv == wave) contract2_body<NB, wave, W, h * W + wave, W * SPLIT>(P, wrow, brow, srow, Gout);
+    });
   });
 }
+// blocks of a sample split over two workgroups from this width on (the
+// compensated accumulators of 8 waves exceed 256 registers above NB = 10)
+constexpr int contract2_split(int nb) { return nb >= 11 ? 2 : 1; }
 
 // ----------------------------------------------------------------------------
 // batched factorisation, MFMA register-blocked: one wave (64 lanes) per unit.
@@ -589,9 +667,11 @@ __global__ __launch_bounds__(64 * W) void contract2_kernel(PsrDev P, const doubl
 // triangle and apply the H panel rows to it; (3) factor A22.  Same
 // arithmetic, re-ordered (left-looking at the 2x2 block level).
 // ----------------------------------------------------------------------------
-template <int NB>
+template <int NB, bool FULL = false>
 struct Split {
-  static constexpr int H = NB == 8 ? 3 : NB / 2;
+  // FULL (dev A/B, one wave per SIMD): the whole triangle resident, plain
+  // right-looking order (phases 2 and 3 empty)
+  static constexpr int H = FULL ? NB : NB == 8 ? 3 : NB / 2;
   static constexpr int M = NB - H;                    // A22 block order
   static constexpr int n1 = H * NB - H * (H - 1) / 2; // blocks (i < H, j >= i)
   static constexpr int n2 = M * (M + 1) / 2;          // blocks (H <= i <= j)
@@ -939,7 +1019,7 @@ static __device__ long long g_stamps[STAMP_UNITS * STAMP_N];
 // noise each distinct spectrum is formed once (the sin / cos columns of a
 // frequency share one: J.rep / J.ulist) and shared through LDS; the last
 // panel's pad pivots are skipped.
-template <int NB, int W, int ALG = PANEL_2L, bool STAMP = false, int KEEP = 0>
+template <int NB, int W, int ALG = PANEL_2L, bool STAMP = false, int KEEP = 0, bool FULL = false>
 __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(W, W)))
 void chol_mfma_kernel(const CholJob* __restrict__ jobs, int B, long long u0, int b_off,
                       const double* __restrict__ theta, int ldth, double* __restrict__ out_units,
@@ -958,9 +1038,10 @@ void chol_mfma_kernel(const CholJob* __restrict__ jobs, int B, long long u0, int
 #endif
   EWH_STAMP(0)
   constexpr int LD = 16 * NB;
-  using S = Split<NB>;
+  using S = Split<NB, FULL>;
   constexpr int H = S::H;
-  static_assert(NB - KEEP >= H, "kept blocks must lie in the phase-3 triangle");
+  static_assert(!FULL || KEEP == 0, "the FULL form has no kept blocks");
+  static_assert(FULL || NB - KEEP >= H, "kept blocks must lie in the phase-3 triangle");
   __shared__ double phinv[LD];
   __shared__ double phs[LD];
   const int lane = threadIdx.x;
@@ -1103,7 +1184,7 @@ void chol_mfma_kernel(const CholJob* __restrict__ jobs, int B, long long u0, int
   });
   // ---- phase 2: A22 -= U12^T U12 ----
   // block by block in row order: U1 column i is dead once row i of A22 is done
-  v4d U2[S::n2];
+  v4d U2[S::n2 > 0 ? S::n2 : 1];
   static_for<H, NB>([&](auto II) {
     constexpr int i = decltype(II)::value;
     static_for<i, NB>([&](auto JJ) {
@@ -1132,7 +1213,9 @@ void chol_mfma_kernel(const CholJob* __restrict__ jobs, int B, long long u0, int
     EWH_STAMP(4 + 2 * bb)
   });
   double qv = 0.0;
-  if constexpr (KEEP == 0) {
+  if constexpr (FULL) {
+    qv = readlane_d(U1[S::i1(NB - 1, NB - 1)][3], 63);
+  } else if constexpr (KEEP == 0) {
     qv = readlane_d(U2[S::i2(NB - 1, NB - 1)][3], 63);
   } else {
     constexpr int KD = 16 * KEEP;
@@ -1183,6 +1266,9 @@ void chol_mfma_kernel(const CholJob* __restrict__ jobs, int B, long long u0, int
 // Same arithmetic as chol_mfma_kernel (right-looking), re-ordered.
 // ----------------------------------------------------------------------------
 constexpr int BIG_NB_MAX = 16;
+// chol_wide_kernel (chol_wide.hip): any width up to WIDE_NB_MAX blocks
+constexpr int WIDE_NB_MAX = 64;
+constexpr int WIDE_LD_MAX = 16 * WIDE_NB_MAX;
 
 template <int NB>
 __device__ __forceinline__ long long big_blk(int p, int j) {   // packed upper block index
@@ -1224,6 +1310,7 @@ void chol_big_kernel(const CholJob* __restrict__ jobs, int B, long long u0, int 
   LogAcc ldet;
   bool ok = true;
   double qv = 0.0;
+  const int klast = __builtin_amdgcn_readfirstlane(J.mreal - 16 * (NB - 1));   // the last row's pad pivots are skipped
   static_for<0, NB>([&](auto I) {
     constexpr int i = decltype(I)::value;
     constexpr int W = NB - i;                       // blocks in row i
@@ -1256,7 +1343,7 @@ void chol_big_kernel(const CholJob* __restrict__ jobs, int B, long long u0, int 
       }
     }
     panel_ldl_row<NB, PANEL_2L, true, true>(I, [&](auto JJ) -> v4d& { return R[decltype(JJ)::value - i]; }, q, c,
-                                            ldet, ok);
+                                            ldet, ok, NoHook{}, klast);
     if constexpr (i < NB - 1) {
       static_for<0, W>([&](auto JJ) {
         constexpr int j = i + decltype(JJ)::value;
@@ -1298,8 +1385,9 @@ constexpr int DCB = 64;            // dense panel width
 
 // ---- launchers defined in the other translation units ----------------------
 // each returns 0 on success (negative EWH_E* on error)
+// Glo: the low part of G (bases past 16 blocks only; may be NULL)
 int launch_contract_nb(int nb, const PsrDev& P, const double* w, const double* beta, const double* s,
-                       const double* fac, double* G, int nb_samples, hipStream_t st);
+                       const double* fac, double* G, int nb_samples, hipStream_t st, double* Glo = nullptr);
 // waves: 4 or 8 per sample (0 = the measured default for nb)
 int launch_contract2_nb(int nb, int waves, const PsrDev& P, const double* w, const double* beta, double* s,
                         long long s_stride, double* G, int nb_samples, hipStream_t st);
@@ -1313,10 +1401,26 @@ int launch_chol_big_nb(int nb, const CholJob* jobs, int B, long long u0, long lo
 // memory; every unit term goes to units[p B + b] and host_units[p B + b].
 // Returns 1 if nb has no latency kernel (caller uses the batched path).
 constexpr int LAT_NB_MAX = 8;
+// unit term of a latency-kernel unit whose dataflow wait ran out (a NaN
+// payload no other path writes; ewh_lnl_batch returns EWH_E_HIP on it)
+constexpr unsigned long long LAT_STALL_BITS = 0x7ff4dead057a1100ull;
 int launch_chol_lat(int nb, const CholJob* jobs, int B, int P, const double* theta, int ldth, double* units,
                     double* host_units, hipStream_t st, bool stamp = false, int var = 0);
+// any width (chol_wide.hip): units [u0, u0 + n), slabs of at most cap
+// workgroups, each with scr_per_wg doubles of scratch (wide_scratch_per_wg);
+// keep > 0: the partial factorisation, kept blocks to keep_out as
+// chol_mfma_kernel<KEEP> writes them
+long long wide_scratch_per_wg(int nb, int keep);
+// double-double factorisation (chol_dd.hip), one 256-thread workgroup per
+// unit, 2 ld^2 doubles of scratch each (dd_scratch_per_wg)
+long long dd_scratch_per_wg(int ld);
+int launch_chol_dd(const CholJob* jobs, int B, long long u0, long long n, int b_off, const double* theta, int ldth,
+                   double* units, double* scr, long long scr_per_wg, long long cap, hipStream_t st);
+int launch_chol_wide(const CholJob* jobs, int B, long long u0, long long n, int b_off, const double* theta, int ldth,
+                     double* units, double* scr, long long scr_per_wg, long long cap, int keep, double* keep_out,
+                     int keep_b0, int keep_bs, hipStream_t st);
 // keep_out: pulsar-major kept blocks, keep_bs samples per pulsar (see chol_mfma_kernel KEEP)
-int launch_partial_nb(int nb, int keep, const CholJob* jobs, int B, long long u0, long long n,
+int launch_partial_nb(int nb, int keep, const CholJob* jobs, int B, long long u0, long long n, int b_off,
                       const double* theta, int ldth, double* units, double* keep_out, int keep_bs, hipStream_t st);
 // dynamic-LDS attributes of the contraction kernels on the current device
 int set_contract_attributes();

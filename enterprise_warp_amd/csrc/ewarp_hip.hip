@@ -101,40 +101,6 @@ __global__ __launch_bounds__(256) void epoch_sums_kernel(PsrDev P, const double*
 }
 
 // ----------------------------------------------------------------------------
-// double-double helpers (Knuth TwoSum, TwoProd by fma; Dekker / Bailey
-// normalisation): value = hi + lo with |lo| <= ulp(hi) / 2
-// ----------------------------------------------------------------------------
-struct dd {
-  double hi, lo;
-};
-__device__ __forceinline__ dd dd_two_sum(double a, double b) {
-  const double s = a + b, bp = s - a;
-  return {s, (a - (s - bp)) + (b - bp)};
-}
-__device__ __forceinline__ dd dd_fast(double a, double b) {   // |a| >= |b|
-  const double s = a + b;
-  return {s, b - (s - a)};
-}
-__device__ __forceinline__ dd dd_add(dd x, dd y) {
-  const dd s = dd_two_sum(x.hi, y.hi);
-  return dd_fast(s.hi, s.lo + x.lo + y.lo);
-}
-__device__ __forceinline__ dd dd_mul(dd x, dd y) {
-  const double p = x.hi * y.hi;
-  return dd_fast(p, fma(x.hi, y.hi, -p) + (x.hi * y.lo + x.lo * y.hi));
-}
-__device__ __forceinline__ dd dd_div(dd x, dd y) {          // one Newton correction of x.hi / y.hi
-  const double q = x.hi / y.hi;
-  const dd r = dd_add(x, dd_mul({-q, 0.0}, y));
-  return dd_fast(q, r.hi / y.hi);
-}
-__device__ __forceinline__ dd dd_sqrt(dd x) {
-  const double r = sqrt(x.hi);
-  const dd e = dd_add(x, dd_mul({-r, 0.0}, {r, 0.0}));
-  return dd_fast(r, e.hi / (2.0 * r));
-}
-
-// ----------------------------------------------------------------------------
 // fixed white noise, one-off (ewh_create / ewh_set_fixed_white): the cached
 // Gram G = T_aug^T W T_aug - sum_e beta_e s_e s_e^T with every entry summed
 // in double-double (Dot2, Ogita-Rump-Oishi 2005: TwoProd by fma, TwoSum) and
@@ -212,7 +178,7 @@ __global__ __launch_bounds__(256) void schur_kernel(double* Ghi, double* Glo, in
                                                     const int* __restrict__ col_ptr,
                                                     const DSpec* __restrict__ spec,
                                                     double Kb, double* S, int fx_ld, int nloc, int gstart,
-                                                    int ncommon, double* Kout, int* fail_out) {
+                                                    int ncommon, double* Kout, int* fail_out, double* Slo) {
   __shared__ double rh[256 * 4], rl[256 * 4];
   __shared__ double red[4];
   double lphi = 0.0;
@@ -262,10 +228,10 @@ __global__ __launch_bounds__(256) void schur_kernel(double* Ghi, double* Glo, in
     const int a = idx / fx_ld, bcol = idx % fx_ld;
     const int ga = gmap(a);
     const int gb = gmap(bcol);
-    double v;
-    if (ga < 0 || gb < 0) v = (a == bcol) ? 1.0 : 0.0;
-    else v = Ghi[(long long)ga * ld + gb] + Glo[(long long)ga * ld + gb];
-    S[idx] = v;
+    dd v = {(a == bcol) ? 1.0 : 0.0, 0.0};
+    if (ga >= 0 && gb >= 0) v = dd_two_sum(Ghi[(long long)ga * ld + gb], Glo[(long long)ga * ld + gb]);
+    S[idx] = v.hi;
+    if (Slo) Slo[idx] = v.lo;     // (the double-double factorisation's input, chol_dd_kernel)
   }
   if (threadIdx.x == 0) {
     *Kout = Kb - logdet - 0.5 * lphi;
@@ -1126,6 +1092,11 @@ struct PsrHost {
   int n_toa = 0, m = 0, nlead = 0, ld = 0, nb = 0, n_epoch = 0;
   int fx_m = 0, fx_ld = 0, fx_nb = 0;
   int ncommon = 0, nloc = 0, gstart = 0;   // correlated layout of the reduced matrix
+  // correlated common process with varying white noise: T_aug is laid out
+  // [lead | own | pad to 16 | common | pad | r] -- common column g at
+  // gstart_v + g, so the partial factorisation keeps whole blocks; the pads
+  // inside take phi = 1 (CONST entries); mreal_v = gstart_v columns take phi^-1
+  int gstart_v = 0;
   PsrDev dev{};
   int* d_colptr = nullptr;        // varying CSR (m+1)
   DSpec* d_spec = nullptr;
@@ -1138,6 +1109,7 @@ struct PsrHost {
   std::vector<int> fx_tidx;       // theta entries the records read (their indices point here); empty: the whole row
   int* d_fx_urep = nullptr;       // fixed columns -> distinct-spectrum record (-1: no entry)
   double* d_S = nullptr;          // fx_ld^2
+  double* d_Slo = nullptr;        // fx_ld^2, the low part of S (dd_path pulsars only)
   bool has_theta_white = false;
   int n_slot = 0;
   ewh_pref* d_slots = nullptr;    // device copy of the white-noise slot table (PsrDev::slots)
@@ -1171,6 +1143,11 @@ struct DevCtx {
   double* d_bigscr = nullptr; // chol_big_kernel: per-workgroup U blocks
   long long bigscr_cap = 0;   // workgroups per launch it holds
   int bigscr_nb = 0;
+  double* d_widescr = nullptr;   // chol_wide_kernel: per-workgroup U blocks
+  long long widescr_len = 0;     // doubles
+  double* d_ddscr = nullptr;     // chol_dd_kernel: per-workgroup hi / lo matrices
+  long long ddscr_len = 0;       // doubles
+  double* d_Glo = nullptr;       // varying white noise, bases past 16 blocks: the low part of G (contract_wide_kernel)
   int chunk = 0;
   int chunk_cap = 0;          // largest chunk the ~1.5 GB scratch budget allows
   int last_B = 0;
@@ -1275,6 +1252,32 @@ void build_csr(const ewh_pulsar_desc& s, int c0, int c1, std::vector<int>& ptr, 
   }
 }
 
+// CSR over T_aug positions for the correlated varying-white-noise layout:
+// basis column c at pos(c), and a CONST phi = 1 entry on each internal pad
+// position [pad0, pad1) (an identity row / column: pivot 1, log phi 0)
+void build_csr_mapped(const ewh_pulsar_desc& s, const std::vector<int>& pos, int ncols, int pad0, int pad1,
+                      std::vector<int>& ptr, std::vector<DSpec>& ent) {
+  ptr.assign(ncols + 1, 0);
+  for (int e = 0; e < s.n_spec; ++e) ptr[pos[s.spec[e].col] + 1]++;
+  for (int a = pad0; a < pad1; ++a) ptr[a + 1]++;
+  for (int j = 0; j < ncols; ++j) ptr[j + 1] += ptr[j];
+  ent.assign(ptr[ncols], DSpec{});
+  std::vector<int> fill(ptr.begin(), ptr.end() - 1);
+  for (int e = 0; e < s.n_spec; ++e) {
+    const int a = pos[s.spec[e].col];
+    ent[fill[a]++] = to_dspec(s.spec[e], a);
+  }
+  for (int a = pad0; a < pad1; ++a) {
+    ewh_spec_entry one{};
+    one.kind = EWH_SPEC_CONST;
+    one.col = a;
+    one.p0 = ewh_pref{-1, 0, 1.0};
+    one.p1 = ewh_pref{-1, 0, 0.0};
+    one.p2 = ewh_pref{-1, 0, 0.0};
+    ent[fill[a]++] = to_dspec(one, a);
+  }
+}
+
 // CSR over the fixed (reduced) layout's fx_ld positions: basis column c >=
 // nlead lands at c - nlead (own) or gstart + (c - nlead - nloc) (common).
 void build_csr_fixed(const ewh_pulsar_desc& s, int nlead, int nloc, int gstart, int fx_ld, std::vector<int>& ptr,
@@ -1323,10 +1326,88 @@ void build_spec_rep(const std::vector<int>& ptr, const std::vector<DSpec>& ent, 
   }
 }
 
-int dispatch_chol(int mode, int nb, int mreal, const CholJob* jobs, int B, long long u0, long long n, int b_off,
-                  const double* theta, int ldth, double* units, hipStream_t st, double* bigscr = nullptr,
-                  long long bigcap = 0) {
+// kernel mode 27: every factorisation (full and partial) by chol_wide_kernel
+// (routing only: the wide kernel is part of the product; tests compare it
+// with the register kernels)
+constexpr int MODE_WIDE = 27;
+
+// The double-double factorisation (chol_dd_kernel) takes the uncorrelated
+// units the fp64 register kernels do not cover with fixed white noise
+// (reduced width > 9 blocks: the cached S is double-double) and every basis
+// wider than 16 blocks; kernel mode 27 routes them to the fp64 chol_wide
+// instead, mode 1 to the LDS kernel (A/B)
+bool dd_path(const DevCtx* h, int nb, bool fixed) {
+  if (h->corr || h->osmode || h->kernel_mode == MODE_WIDE || h->kernel_mode == 1) return false;
+  return nb > BIG_NB_MAX || (fixed && nb > MFMA_NB_MAX);
+}
+
+long long ensure_dd_scratch(DevCtx* h, int ld) {
+  const long long per = dd_scratch_per_wg(ld);
+  const long long want = std::min<long long>(1024, std::max<long long>(1, (1LL << 27) / per)) * per;
+  if (h->ddscr_len < want) {
+    if (h->d_ddscr) {
+      (void)hipFree(h->d_ddscr);
+      h->allocs.erase(std::find(h->allocs.begin(), h->allocs.end(), (void*)h->d_ddscr));
+      h->d_ddscr = nullptr;
+    }
+    h->ddscr_len = 0;
+    if (dalloc(h, &h->d_ddscr, (size_t)want)) return 0;
+    h->ddscr_len = want;
+  }
+  return std::min<long long>(1024, h->ddscr_len / per);
+}
+
+// scratch of chol_wide_kernel for (nb, keep): workgroups per launch it holds
+// (0: allocation failed); at most 2048 workgroups, ~1 GB
+long long ensure_wide_scratch(DevCtx* h, int nb, int keep) {
+  const long long per = wide_scratch_per_wg(nb, keep);
+  const long long want = std::min<long long>(2048, std::max<long long>(1, (1LL << 27) / per)) * per;
+  if (h->widescr_len < want) {
+    if (h->d_widescr) {
+      (void)hipFree(h->d_widescr);
+      h->allocs.erase(std::find(h->allocs.begin(), h->allocs.end(), (void*)h->d_widescr));
+      h->d_widescr = nullptr;
+    }
+    h->widescr_len = 0;
+    if (dalloc(h, &h->d_widescr, (size_t)want)) return 0;
+    h->widescr_len = want;
+  }
+  return std::min<long long>(2048, h->widescr_len / per);
+}
+
+int launch_wide(DevCtx* h, int nb, int keep, const CholJob* jobs, int B, long long u0, long long n, int b_off,
+                const double* theta, int ldth, double* units, double* keep_out, hipStream_t st) {
+  if (nb > WIDE_NB_MAX) return set_err(EWH_E_UNSUPPORTED, "basis wider than 1023 columns");
+  const long long cap = ensure_wide_scratch(h, nb, keep);
+  if (cap <= 0) return EWH_E_NOMEM;
+  return launch_chol_wide(jobs, B, u0, n, b_off, theta, ldth, units, h->d_widescr, wide_scratch_per_wg(nb, keep), cap,
+                          keep, keep_out, 0, B, st);
+}
+
+// the partial factorisation (correlated common process) of units [u0, u0 + n)
+// of one run of pulsars with nb blocks: the register kernel where it fits
+// (chol_mfma_kernel<NB <= 9, KEEP>, phase split permitting), else chol_wide
+int partial_units(DevCtx* h, const CholJob* jobs, int nb, int B, long long u0, long long n, int b_off,
+                  const double* theta, double* units, double* keep_out, hipStream_t st) {
+  const bool regs = nb <= MFMA_NB_MAX && nb - h->keep >= (nb == 8 ? 3 : nb / 2);
+  if (regs && h->kernel_mode != MODE_WIDE)
+    return launch_partial_nb(nb, h->keep, jobs, B, u0, n, b_off, theta, h->n_param, units, keep_out, B, st);
+  return launch_wide(h, nb, h->keep, jobs, B, u0, n, b_off, theta, h->n_param, units, keep_out, st);
+}
+
+int dispatch_chol(DevCtx* h, int nb, int mreal, const CholJob* jobs, int B, long long u0, long long n, int b_off,
+                  const double* theta, int ldth, double* units, hipStream_t st, bool fixed) {
   if (n <= 0) return 0;
+  const int mode = h->kernel_mode;
+  if (dd_path(h, nb, fixed)) {
+    const long long cap = ensure_dd_scratch(h, 16 * nb);
+    if (cap <= 0) return EWH_E_NOMEM;
+    return launch_chol_dd(jobs, B, u0, n, b_off, theta, ldth, units, h->d_ddscr, dd_scratch_per_wg(16 * nb), cap, st);
+  }
+  if (mode == MODE_WIDE || nb > BIG_NB_MAX)
+    return launch_wide(h, nb, 0, jobs, B, u0, n, b_off, theta, ldth, units, nullptr, st);
+  double* bigscr = h->d_bigscr;
+  const long long bigcap = h->bigscr_cap;
   if (mode != 1 && nb > MFMA_NB_MAX && nb <= BIG_NB_MAX && bigscr)
     return launch_chol_big_nb(nb, jobs, B, u0, n, b_off, theta, ldth, units, bigscr, bigcap, st);
   if (mode != 1 && nb <= MFMA_NB_MAX) {
@@ -1375,7 +1456,8 @@ int ensure_var_scratch(DevCtx* h, int B) {
   // reuse while the chunk covers the batch or already sits at its cap (the
   // memory-derived limit, at most 1024): no free / re-malloc per call
   if (h->chunk > 0 && (h->chunk >= B || h->chunk >= h->chunk_cap)) return 0;
-  for (void* p : {(void*)h->d_w, (void*)h->d_beta, (void*)h->d_s, (void*)h->d_G, (void*)h->d_Kb, (void*)h->d_fac}) {
+  for (void* p : {(void*)h->d_w, (void*)h->d_beta, (void*)h->d_s, (void*)h->d_G, (void*)h->d_Kb, (void*)h->d_fac,
+                  (void*)h->d_Glo}) {
     if (p) {
       (void)hipFree(p);
       h->allocs.erase(std::find(h->allocs.begin(), h->allocs.end(), p));
@@ -1392,24 +1474,33 @@ int ensure_var_scratch(DevCtx* h, int B) {
   // epoch-sum rows per sample: whole CT_ROWS tiles (+1) so the pipelined
   // contraction's last epoch tile reads zero-initialised pad rows
   const size_t sstride = ((maxe + CT_ROWS - 1) / CT_ROWS + 1) * CT_ROWS * maxld;
-  const size_t per = (maxld * maxld + sstride + maxn + maxe + maxfac + 1) * sizeof(double);
+  const bool wide = maxld > 16 * BIG_NB_MAX;        // G_lo for the double-double factorisation
+  const size_t per = ((wide ? 2 : 1) * maxld * maxld + 2 * sstride + maxn + maxe + maxfac + 1) * sizeof(double);
   const size_t cap = std::min<size_t>(1024, std::max<size_t>(1, (size_t)1536 * 1024 * 1024 / per));
   h->chunk_cap = (int)cap;
   const size_t chunk = std::min<size_t>(cap, (size_t)std::max(B, 1));
   int rc;
   if ((rc = dalloc(h, &h->d_w, chunk * maxn))) return rc;
   if ((rc = dalloc(h, &h->d_beta, chunk * maxe))) return rc;
-  if ((rc = dalloc(h, &h->d_s, chunk * sstride))) return rc;
-  EWH_HIP(hipMemset(h->d_s, 0, chunk * sstride * sizeof(double)));
+  // (x2: contract2_kernel with its blocks split over two workgroups per
+  // sample keeps one epoch-sum row per half)
+  if ((rc = dalloc(h, &h->d_s, 2 * chunk * sstride))) return rc;
+  EWH_HIP(hipMemset(h->d_s, 0, 2 * chunk * sstride * sizeof(double)));
   h->s_stride = (long long)sstride;
   if ((rc = dalloc(h, &h->d_G, chunk * maxld * maxld))) return rc;
   if ((rc = dalloc(h, &h->d_Kb, chunk))) return rc;
   if ((rc = dalloc(h, &h->d_fac, chunk * maxfac))) return rc;
+  h->d_Glo = nullptr;
+  if (wide && (rc = dalloc(h, &h->d_Glo, chunk * maxld * maxld))) return rc;
   h->chunk = (int)chunk;
   std::vector<CholJob> jobs(h->P);
   for (int p = 0; p < h->P; ++p) {
     const PsrHost& ps = h->psr[p];
-    jobs[p] = CholJob{h->d_G, (long long)ps.ld * ps.ld, ps.ld, ps.m, ps.d_colptr, ps.d_spec, h->d_Kb, 1, 0};
+    // (correlated: the columns before the common block take phi^-1; the
+    // common block is assembled globally)
+    const int mreal = h->corr ? ps.gstart_v : ps.m;
+    jobs[p] = CholJob{h->d_G, (long long)ps.ld * ps.ld, ps.ld, mreal, ps.d_colptr, ps.d_spec, h->d_Kb, 1, 0};
+    if (ps.nb > BIG_NB_MAX) jobs[p].mats_lo = h->d_Glo;
   }
   EWH_HIP(hipMemcpy(h->d_jobs_var, jobs.data(), sizeof(CholJob) * h->P, hipMemcpyHostToDevice));
   return 0;
@@ -1431,7 +1522,8 @@ int run_white(DevCtx* h, int p, const double* theta, int ldth, int b0, int nb) {
   if (ps.n_epoch > 0)
     hipLaunchKernelGGL(epoch_sums_kernel, dim3(ps.n_epoch, nb), dim3(256), 0, h->stream, ps.dev, h->d_w, h->d_fac,
                        h->d_s);
-  int rc = launch_contract_nb(ps.nb, ps.dev, h->d_w, h->d_beta, h->d_s, h->d_fac, h->d_G, nb, h->stream);
+  int rc = launch_contract_nb(ps.nb, ps.dev, h->d_w, h->d_beta, h->d_s, h->d_fac, h->d_G, nb, h->stream,
+                              ps.nb > BIG_NB_MAX ? h->d_Glo : nullptr);
   if (rc) return rc;
   EWH_HIP(hipGetLastError());
   return 0;
@@ -1495,9 +1587,12 @@ int setup_fixed(DevCtx* h) {
     EWH_HIP(hipMemcpyAsync(&Kb_h, Kb, sizeof(double), hipMemcpyDeviceToHost, h->stream));
     EWH_HIP(hipStreamSynchronize(h->stream));
     if (!ps.d_S && (rc = dalloc(h, &ps.d_S, (size_t)ps.fx_ld * ps.fx_ld))) return rc;
+    // the low part of S for the double-double factorisation (uncorrelated
+    // bases past the register kernels, dd_path)
+    if (!ps.d_Slo && dd_path(h, ps.fx_nb, true) && (rc = dalloc(h, &ps.d_Slo, (size_t)ps.fx_ld * ps.fx_ld))) return rc;
     hipLaunchKernelGGL(schur_kernel, dim3(1), dim3(256), 0, h->stream, G, Glo, ps.ld, ps.m, ps.nlead, ps.d_colptr,
                        ps.d_spec, Kb_h, ps.d_S, ps.fx_ld, ps.nloc, ps.gstart, ps.ncommon, h->d_fxK + p,
-                       h->d_fxfail + p);
+                       h->d_fxfail + p, ps.d_Slo);
     EWH_HIP(hipGetLastError());
     // mreal: columns that take phi^-1 in the factorisation -- the own columns
     // (correlated: the common block is assembled globally), or every column
@@ -1505,6 +1600,7 @@ int setup_fixed(DevCtx* h) {
     const int mreal = h->osmode ? ps.fx_ld - 1 : ps.nloc;
     jobs[p] = CholJob{ps.d_S, 0, ps.fx_ld, mreal, ps.d_fx_colptr, ps.d_fx_spec, h->d_fxK + p, 0, 0,
                       ps.d_fx_rep, ps.d_fx_ulist, ps.fx_nu, h->stage_spectra ? ps.d_fx_urec : nullptr, ps.d_fx_urep};
+    jobs[p].mats_lo = ps.d_Slo;
     if (jobs[p].urec != nullptr) {
       jobs[p].ntidx = (int)ps.fx_tidx.size();
       for (int i = 0; i < jobs[p].ntidx; ++i) jobs[p].tidx[i] = ps.fx_tidx[i];
@@ -1524,16 +1620,24 @@ int setup_common(DevCtx* h, const ewh_pta_desc* d) {
   h->nc = c.n_col;
   h->keep = (c.n_col + 1 + 15) / 16;
   for (auto& ps : h->psr) {
-    if (ps.fx_nb - ps.gstart / 16 != h->keep) return set_err(EWH_E_INVALID, "common: inconsistent reduced layout");
-    if (ps.fx_nb > MFMA_NB_MAX || ps.fx_nb - h->keep < ps.fx_nb / 2 || (ps.fx_nb == 8 && ps.fx_nb - h->keep < 3))
-      return set_err(EWH_E_UNSUPPORTED, "common: reduced basis too wide for the partial register factorisation");
+    const int nbk = h->white_fixed ? ps.fx_nb : ps.nb;
+    const int gs = h->white_fixed ? ps.gstart : ps.gstart_v;
+    if (nbk - gs / 16 != h->keep) return set_err(EWH_E_INVALID, "common: inconsistent reduced layout");
+    if (nbk > WIDE_NB_MAX) return set_err(EWH_E_UNSUPPORTED, "common: basis wider than 1023 columns");
   }
   int rc;
   if ((rc = dupload(h, &h->d_orf, c.orf, (size_t)P * P))) return rc;
+  // per pulsar: the CSR whose positions gstart.. hold the common columns'
+  // own entries (fixed white noise: the reduced layout; varying: T_aug's)
+  auto common_psr = [&](int p) {
+    const PsrHost& ps = h->psr[p];
+    return h->white_fixed ? CommonPsr{ps.d_fx_colptr, ps.d_fx_spec, ps.gstart, 0}
+                          : CommonPsr{ps.d_colptr, ps.d_spec, ps.gstart_v, 0};
+  };
   if (h->osmode) {               // optimal statistic: the CURN likelihood layout + the ORF only
     h->corr = false;
     std::vector<CommonPsr> cps(P);
-    for (int p = 0; p < P; ++p) cps[p] = CommonPsr{h->psr[p].d_fx_colptr, h->psr[p].d_fx_spec, h->psr[p].gstart, 0};
+    for (int p = 0; p < P; ++p) cps[p] = common_psr(p);
     return dupload(h, &h->d_cps, cps.data(), cps.size());
   }
   std::vector<DSpec> cs(c.n_col);
@@ -1577,7 +1681,7 @@ int setup_common(DevCtx* h, const ewh_pta_desc* d) {
   if ((rc = dupload(h, &h->d_cuniq, uniq.data(), uniq.size()))) return rc;
   if ((rc = dupload(h, &h->d_crep, rep.data(), rep.size()))) return rc;
   std::vector<CommonPsr> cps(P);
-  for (int p = 0; p < P; ++p) cps[p] = CommonPsr{h->psr[p].d_fx_colptr, h->psr[p].d_fx_spec, h->psr[p].gstart, 0};
+  for (int p = 0; p < P; ++p) cps[p] = common_psr(p);
   if ((rc = dupload(h, &h->d_cps, cps.data(), cps.size()))) return rc;
   h->Np = DCB * ((P * h->nc + 1 + DCB - 1) / DCB);
   const double per = (double)h->Np * h->Np * 8.0;
@@ -1635,15 +1739,31 @@ int ensure_keep(DevCtx* h, int B) {
 int corr_partial(DevCtx* h, const double* theta_dev, int B, int p_begin, int p_end, double* units, double* keep,
                  hipStream_t st) {
   int rc;
+  if (!h->white_fixed) {
+    // white noise varying: per pulsar and sample chunk the contraction
+    // (run_white: N^-1, ECORR, G = T_aug^T N^-1 T_aug on h->stream) and the
+    // partial factorisation of G + diag(phi^-1) with the timing model in
+    if ((rc = ensure_var_scratch(h, B))) return rc;
+    hipStream_t saved = h->stream;
+    h->stream = st;
+    for (int p = p_begin; p < p_end && !rc; ++p)
+      for (int c0 = 0; c0 < B && !rc; c0 += h->chunk) {
+        const int nb = std::min(h->chunk, B - c0);
+        rc = run_white(h, p, theta_dev, h->n_param, c0, nb);
+        if (!rc)
+          rc = partial_units(h, h->d_jobs_var, h->psr[p].nb, B, (long long)p * B + c0, nb, c0, theta_dev, units, keep,
+                             st);
+      }
+    h->stream = saved;
+    return rc;
+  }
   for (long long u = (long long)p_begin * B; u < (long long)p_end * B;) {
     const int p0 = (int)(u / B);
     const int nb0 = h->psr[p0].fx_nb;
     int p1 = p0 + 1;
     while (p1 < p_end && h->psr[p1].fx_nb == nb0) ++p1;
     const long long seg_end = (long long)p1 * B;
-    if ((rc = launch_partial_nb(nb0, h->keep, h->d_jobs_fixed, B, u, seg_end - u, theta_dev, h->n_param, units,
-                                keep, B, st)))
-      return rc;
+    if ((rc = partial_units(h, h->d_jobs_fixed, nb0, B, u, seg_end - u, 0, theta_dev, units, keep, st))) return rc;
     u = seg_end;
   }
   return 0;
@@ -1876,11 +1996,33 @@ int create_ctx(const ewh_pta_desc* d, const std::vector<ProjCoef>& proj, int dev
   bool any_theta_white = false;
   for (int p = 0; p < h->P; ++p) {
     const ewh_pulsar_desc& s = d->pulsars[p];
+    for (int i = 0; i < s.n_slot; ++i) any_theta_white |= pref_uses_theta(s.slots[i]);
+    any_theta_white |= s.n_bgroup > 0;
+  }
+  // a correlated common process with white noise varying (or a theta-dependent
+  // basis): per sample, the contraction of a T_aug laid out with the common
+  // columns in whole blocks, then the partial factorisation (corr_partial)
+  const bool corr_var = d->common && d->common->kind == EWH_COMMON_CORRELATED &&
+                        !((d->white_fixed != 0) && !any_theta_white);
+  for (int p = 0; p < h->P; ++p) {
+    const ewh_pulsar_desc& s = d->pulsars[p];
     PsrHost& ps = h->psr[p];
     ps.n_toa = s.n_toa;
     ps.m = s.n_col;
     ps.nlead = s.n_lead_const;
-    ps.nb = nb_for(s.n_col + 1);
+    // T_aug position of basis column j (identity, or the corr_var layout)
+    std::vector<int> vpos(s.n_col);
+    for (int j = 0; j < s.n_col; ++j) vpos[j] = j;
+    int pad0 = 0, pad1 = 0;
+    if (corr_var) {
+      const int nlo = s.n_col - s.n_common;
+      ps.gstart_v = 16 * ((nlo + 15) / 16);
+      for (int j = nlo; j < s.n_col; ++j) vpos[j] = ps.gstart_v + (j - nlo);
+      pad0 = nlo;
+      pad1 = ps.gstart_v;
+      ps.m = ps.gstart_v + s.n_common;
+    }
+    ps.nb = nb_for(ps.m + 1);
     ps.ld = 16 * ps.nb;
     ps.n_epoch = s.n_epoch;
     ps.fx_m = s.n_col - s.n_lead_const;
@@ -1895,7 +2037,6 @@ int create_ctx(const ewh_pta_desc* d, const std::vector<ProjCoef>& proj, int dev
     }
     ps.fx_ld = 16 * ps.fx_nb;
     for (int i = 0; i < s.n_slot; ++i) ps.has_theta_white |= pref_uses_theta(s.slots[i]);
-    any_theta_white |= ps.has_theta_white || s.n_bgroup > 0;
     // T_aug: [basis | 0-pad | r], row-major n x ld
     // (+CT_ROWS zero rows: the pipelined contraction copies whole tiles)
     std::vector<double> Ta((size_t)(s.n_toa + CT_ROWS) * ps.ld, 0.0), sig2(s.n_toa);
@@ -1905,6 +2046,16 @@ int create_ctx(const ewh_pta_desc* d, const std::vector<ProjCoef>& proj, int dev
       sig2[t] = s.toaerr[t] * s.toaerr[t];
     }
     apply_projection(proj[p], s.n_toa, ps.ld, Ta);
+    if (corr_var) {       // common columns to their block-aligned positions (from the top: pos >= j)
+      for (int t = 0; t < s.n_toa; ++t) {
+        double* row = &Ta[(size_t)t * ps.ld];
+        for (int j = s.n_col - 1; j >= pad0; --j) {
+          const double v = row[j];
+          row[j] = 0.0;
+          row[vpos[j]] = v;
+        }
+      }
+    }
     double* dT;
     double* dsig2;
     int *d_ef, *d_eq, *d_es, *d_ee, *d_eslot;
@@ -1928,16 +2079,17 @@ int create_ctx(const ewh_pta_desc* d, const std::vector<ProjCoef>& proj, int dev
     ewh_pref* d_bg = nullptr;
     if (s.n_bgroup > 0) {
       std::vector<int> cbg(ps.ld, -1);
-      for (int j = 0; j < s.n_col; ++j) cbg[j] = s.col_bgroup[j];
+      for (int j = 0; j < s.n_col; ++j) cbg[vpos[j]] = s.col_bgroup[j];
       if ((rc = dupload(h, &d_cbg, cbg.data(), cbg.size()))) return bail(rc);
       if ((rc = dupload(h, &d_lnc, s.ln_chrom, (size_t)s.n_toa))) return bail(rc);
       if ((rc = dupload(h, &d_bg, s.bgroup_idx, (size_t)s.n_bgroup))) return bail(rc);
     }
-    ps.dev = PsrDev{s.n_toa, s.n_col, ps.ld, ps.nb, s.n_epoch, dT, dsig2, d_ef, d_eq, ps.d_slots, d_es, d_ee, d_eslot,
+    ps.dev = PsrDev{s.n_toa, ps.m, ps.ld, ps.nb, s.n_epoch, dT, dsig2, d_ef, d_eq, ps.d_slots, d_es, d_ee, d_eslot,
                     s.n_bgroup, d_cbg, d_lnc, d_bg, d_tep};
     std::vector<int> ptr;
     std::vector<DSpec> ent;
-    build_csr(s, 0, s.n_col, ptr, ent);
+    if (corr_var) build_csr_mapped(s, vpos, ps.m, pad0, pad1, ptr, ent);
+    else build_csr(s, 0, s.n_col, ptr, ent);
     if ((rc = dupload(h, &ps.d_colptr, ptr.data(), ptr.size()))) return bail(rc);
     if ((rc = dupload(h, &ps.d_spec, ent.data(), ent.size()))) return bail(rc);
     build_csr_fixed(s, ps.nlead, ps.nloc, ps.gstart, ps.fx_ld, ptr, ent);
@@ -1994,8 +2146,8 @@ int create_ctx(const ewh_pta_desc* d, const std::vector<ProjCoef>& proj, int dev
   if ((rc = dalloc(h, &h->d_jobs_fixed, h->P))) return bail(rc);
   if ((rc = dalloc(h, &h->d_jobs_var, h->P))) return bail(rc);
   h->osmode = d->common && d->common->kind == EWH_COMMON_OPTSTAT;
-  if (d->common && !h->white_fixed)
-    return bail(set_err(EWH_E_UNSUPPORTED, "correlated common process: white noise must be fixed (TNT cached)"));
+  if (h->osmode && !h->white_fixed)
+    return bail(set_err(EWH_E_UNSUPPORTED, "optimal statistic: white noise must be fixed (TNT cached)"));
   if (h->white_fixed && (rc = setup_fixed(h))) return bail(rc);
   if (d->common && (rc = setup_common(h, d))) return bail(rc);
   if (h->white_fixed && !h->corr && !h->osmode) {
@@ -2044,8 +2196,8 @@ int ctx_units(DevCtx* h, const double* theta_dev, int B, int64_t u_begin, int64_
       int maxm = 0;
       for (int p = p0; p < p1; ++p) maxm = std::max(maxm, h->psr[p].fx_m);
       if ((rc = ensure_big_scratch(h, nb0)) ||
-          (rc = dispatch_chol(h->kernel_mode, nb0, maxm, h->d_jobs_fixed, B, u, seg_end - u, 0, theta_dev, ldth,
-                              h->d_units, st, h->d_bigscr, h->bigscr_cap)))
+          (rc = dispatch_chol(h, nb0, maxm, h->d_jobs_fixed, B, u, seg_end - u, 0, theta_dev, ldth, h->d_units, st,
+                              true)))
         return rc;
       u = seg_end;
     }
@@ -2059,8 +2211,8 @@ int ctx_units(DevCtx* h, const double* theta_dev, int B, int64_t u_begin, int64_
         const int nb = std::min(h->chunk, be - c0);
         if ((rc = run_white(h, p, theta_dev, ldth, c0, nb))) return rc;
         if ((rc = ensure_big_scratch(h, h->psr[p].nb)) ||
-            (rc = dispatch_chol(h->kernel_mode, h->psr[p].nb, h->psr[p].m, h->d_jobs_var, B, (long long)p * B + c0, nb,
-                                c0, theta_dev, ldth, h->d_units, st, h->d_bigscr, h->bigscr_cap)))
+            (rc = dispatch_chol(h, h->psr[p].nb, h->psr[p].m, h->d_jobs_var, B, (long long)p * B + c0, nb, c0,
+                                theta_dev, ldth, h->d_units, st, false)))
           return rc;
       }
       u = pend;
@@ -2175,8 +2327,7 @@ int ctx_optstat(DevCtx* h, const double* theta_host, int32_t B, const double* ph
     int p1 = p0 + 1;
     while (p1 < P && h->psr[p1].fx_nb == nb0) ++p1;
     const long long seg_end = (long long)p1 * B;
-    if ((rc = launch_partial_nb(nb0, h->keep, h->d_jobs_fixed, B, u, seg_end - u, th, h->n_param, h->d_units,
-                                h->d_keep, B, st))) {
+    if ((rc = partial_units(h, h->d_jobs_fixed, nb0, B, u, seg_end - u, 0, th, h->d_units, h->d_keep, st))) {
       release();
       return rc;
     }
@@ -2235,8 +2386,11 @@ struct ewh_handle {
 
 namespace {
 
-int ensure_pinned(double** p, size_t* cap, size_t need) {
+// cached: the latency path's record of which host buffer its device address
+// belongs to -- cleared on reallocation (a new buffer may reuse the address)
+int ensure_pinned(double** p, size_t* cap, size_t need, const double** cached = nullptr) {
   if (need <= *cap) return 0;
+  if (cached) *cached = nullptr;
   if (*p) (void)hipHostFree(*p);
   *p = nullptr;
   *cap = 0;
@@ -2280,7 +2434,7 @@ int lnl_batch_corr_pulsars(ewh_handle* H, int B, double* out_host) {
   DevCtx* h0 = H->ctx[0];
   const size_t kd2 = (size_t)(16 * h0->keep) * (16 * h0->keep);
   int rc;
-  if ((rc = ensure_pinned(&H->h_out, &H->h_out_cap, (size_t)B))) return rc;
+  if ((rc = ensure_pinned(&H->h_out, &H->h_out_cap, (size_t)B, &H->lat_out_host))) return rc;
   for (int i = 0; i < nd; ++i) {
     DevCtx* h = H->ctx[i];
     EWH_HIP(hipSetDevice(h->device));
@@ -2337,12 +2491,12 @@ constexpr int LAT_B_MAX = 8;    // batches up to this size take the latency kern
 int lnl_batch_single(ewh_handle* H, DevCtx* h, int B, double* out_host) {
   int rc;
   EWH_HIP(hipSetDevice(h->device));
-  if ((rc = ensure_pinned(&H->h_out, &H->h_out_cap, (size_t)B))) return rc;
+  if ((rc = ensure_pinned(&H->h_out, &H->h_out_cap, (size_t)B, &H->lat_out_host))) return rc;
   const int km = h->kernel_mode;
-  if (h->lat_nb > 0 && B <= LAT_B_MAX && (km == 0 || km == 22 || km == 24 || km == 25)) {
+  if (h->lat_nb > 0 && B <= LAT_B_MAX && (km == 0 || km == 22 || km == 23 || km == 24 || km == 25)) {
     // latency path: one launch reads theta from the pinned staging and writes
     // the unit terms to pinned memory (chol_lat.hip); the host folds them
-    if ((rc = ensure_units(h, B)) || (rc = ensure_pinned(&H->h_out, &H->h_out_cap, (size_t)h->P * B))) return rc;
+    if ((rc = ensure_units(h, B)) || (rc = ensure_pinned(&H->h_out, &H->h_out_cap, (size_t)h->P * B, &H->lat_out_host))) return rc;
     // device addresses of the pinned staging (looked up again only after a reallocation)
     if (H->lat_th_host != H->h_theta) {
       EWH_HIP(hipHostGetDevicePointer((void**)&H->lat_th_dev, H->h_theta, 0));
@@ -2363,7 +2517,7 @@ int lnl_batch_single(ewh_handle* H, DevCtx* h, int B, double* out_host) {
     volatile uint64_t* hu = reinterpret_cast<volatile uint64_t*>(H->h_out);
     for (size_t i = 0; i < nu; ++i) hu[i] = LAT_SENTINEL;
     if ((rc = launch_chol_lat(h->lat_nb, h->d_jobs_fixed, B, h->P, th_dev, h->n_param, h->d_units, out_dev,
-                              h->stream, km == 22, km == 24 ? 1 : km == 25 ? 2 : 0)) < 0)
+                              h->stream, km == 22, km == 24 ? 1 : km == 25 ? 2 : km == 23 ? 3 : 0)) < 0)
       return rc;
     if (rc == 0) {
       const auto t0 = std::chrono::steady_clock::now();
@@ -2385,6 +2539,14 @@ int lnl_batch_single(ewh_handle* H, DevCtx* h, int B, double* out_host) {
         }
       }
       std::atomic_thread_fence(std::memory_order_acquire);
+      // a unit whose dataflow wait ran out carries LAT_STALL_BITS: an error,
+      // never a NaN lnL (the ABI promises finite values or -inf)
+      for (size_t i = 0; i < nu; ++i)
+        if (hu[i] == LAT_STALL_BITS) {
+          (void)hipStreamSynchronize(h->stream);
+          return set_err(EWH_E_HIP, "chol_lat_kernel: a dataflow wait of unit " + std::to_string(i) +
+                                        " ran out (LAT_SPIN_MAX); no lnL was produced");
+        }
       // lnL_b = sum over pulsars in pulsar order (reduce_units_kernel's fold)
       for (int b = 0; b < B; ++b) {
         double s = 0.0;
@@ -2504,7 +2666,7 @@ int ewh_set_fixed_white(ewh_handle* H, const double* values) {
 
 int ewh_set_kernel_mode(ewh_handle* H, int32_t mode) {
   if (!H || mode < 0 || mode > 30) return set_err(EWH_E_INVALID, "bad handle / mode");
-  if (mode != 0 && mode != 1 && mode != 2 && mode != 7 && !variant_built(mode))
+  if (mode != 0 && mode != 1 && mode != 2 && mode != 7 && mode != MODE_WIDE && !variant_built(mode))
     return set_err(EWH_E_UNSUPPORTED, "kernel mode " + std::to_string(mode) +
                                           " is not built into this library (A/B variants: the dev library, make dev)");
   for (DevCtx* h : H->ctx) {
@@ -2545,7 +2707,7 @@ int ewh_lnl_batch(ewh_handle* H, const double* theta_host, int32_t B, double* ou
   if (H->ctx[0]->osmode) return set_err(EWH_E_UNSUPPORTED, "an optimal-statistic handle evaluates ewh_optstat only");
   const int nd = (int)H->ctx.size(), np = H->n_param;
   int rc;
-  if ((rc = ensure_pinned(&H->h_theta, &H->h_theta_cap, (size_t)B * std::max(1, np)))) return rc;
+  if ((rc = ensure_pinned(&H->h_theta, &H->h_theta_cap, (size_t)B * std::max(1, np), &H->lat_th_host))) return rc;
   if (np > 0) std::memcpy(H->h_theta, theta_host, sizeof(double) * (size_t)B * np);
   if (nd == 1) return lnl_batch_single(H, H->ctx[0], B, out_host);
   if (H->corr && B < nd) return lnl_batch_corr_pulsars(H, B, out_host);
@@ -2559,7 +2721,7 @@ int ewh_lnl_batch(ewh_handle* H, const double* theta_host, int32_t B, double* ou
     for (int p = 0; p < H->P; ++p) cost[p] = ctx_unit_cost(H->ctx[0], p);
     split = unit_ranges(cost, B, nd);
   }
-  if ((rc = ensure_pinned(&H->h_out, &H->h_out_cap, (size_t)B))) return rc;
+  if ((rc = ensure_pinned(&H->h_out, &H->h_out_cap, (size_t)B, &H->lat_out_host))) return rc;
   DevCtx* h0 = H->ctx[0];
   if (!H->corr) {
     // per-context partial sums are folded on the first device: a partial

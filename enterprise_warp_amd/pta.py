@@ -410,6 +410,8 @@ class Engine:
     def lnl_batch(self, theta):
         theta = np.ascontiguousarray(theta, dtype=float)
         B = theta.shape[0]
+        if not self.h:
+            raise _lib.EngineError("engine is closed")
         if B <= self.SMALL_B and self.n_param > 0:
             self._small[:B] = theta
             h, tp, op = self._small_args
@@ -507,6 +509,10 @@ class Engine:
         _lib.check(self.lib.ewh_set_kernel_mode(self.h, int(mode)))
 
     def close(self):
+        # (the small-batch path's bound arguments hold the raw handle: drop
+        # them with it, so a closed engine raises instead of passing a freed
+        # handle to ewh_lnl_batch)
+        self._small_args = None
         if getattr(self, "h", None):
             self.lib.ewh_destroy(self.h)
             self.h = None

@@ -299,9 +299,12 @@ def config_c4(n_psr=30, n_min=1000, n_max=12000, seed=30, epoch_size=16):
     return SimpleNamespace(name="C4", pta=pta, truth=truth, B=1024, theta_seed=seed)
 
 
-def config_c5(n_psr=100, n_toa=20000, seed=100, epoch_size=16, gwb="hd_vary_gamma_14_nfreqs", nfreqs=30):
+def config_c5(n_psr=100, n_toa=20000, seed=100, epoch_size=16, gwb="hd_vary_gamma_14_nfreqs", nfreqs=30,
+              fixed_white=True):
     """BASELINE config 5: n_psr x n_toa PTA, fixed white noise + ECORR, red and
-    DM noise, and a Hellings-Downs correlated GWB (cross-pulsar Sigma)."""
+    DM noise, and a Hellings-Downs correlated GWB (cross-pulsar Sigma).
+    fixed_white=False: efac / equad / ecorr sampled (enterprise_models.py:
+    108-146 stacked under the correlated process, :390-403)."""
     rng = np.random.default_rng(seed)
     psrs = []
     for i in range(n_psr):
@@ -309,11 +312,11 @@ def config_c5(n_psr=100, n_toa=20000, seed=100, epoch_size=16, gwb="hd_vary_gamm
         psrs.append(make_pulsar(f"J{i:04d}+{seed:04d}", int(n_toa), seed=seed * 1000 + i, pos=v / np.linalg.norm(v),
                                 epoch_size=epoch_size))
     Tspan = max(p.toas.max() for p in psrs) - min(p.toas.min() for p in psrs)
-    ns = params_namespace(Tspan, True)
+    ns = params_namespace(Tspan, fixed_white)
     wn = white_noisedict(psrs, seed + 1)
     terms = {"efac": "by_backend", "equad": "by_backend", "ecorr": "by_backend",
              "spin_noise": f"powerlaw_{nfreqs}_nfreqs", "dm_noise": f"powerlaw_{nfreqs}_nfreqs"}
-    pta = build_pta(psrs, terms, {"gwb": gwb}, ns, wn)
+    pta = build_pta(psrs, terms, {"gwb": gwb}, ns, wn if fixed_white else None)
     truth = truth_values(pta, seed + 2, white=wn)
     simulate_residuals(pta, truth, seed + 3)
     return SimpleNamespace(name="C5", pta=pta, truth=truth, B=512, theta_seed=seed, terms=terms,

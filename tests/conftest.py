@@ -169,7 +169,7 @@ def load_golden(name, full=False):
 
 
 GOLDEN_NAMES = ["c1_j1832", "c1_turnover", "c1_system", "c2_small", "c2_chromvary", "c3_small", "c3_freesp",
-                "c4_small", "c5_small", "c5_mono", "c5_noauto", "c5_dipo"]
+                "c4_small", "c5_small", "c5_mono", "c5_noauto", "c5_dipo", "c5_varwn", "c1_wide", "c1_widefix"]
 
 
 def gpu_available():

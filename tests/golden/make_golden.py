@@ -209,6 +209,31 @@ def main():
     X = np.vstack([synth.prior_draws(pta_s, 8, 19), synth.near_draws(pta_s, truth_s, 8, 20)])
     dump("c1_system", pta_s, {"per_psr_terms": terms_s, "common_terms": {}, "Tspan": float(np.ptp(psr.toas)),
                               "fixed_white": True, "noisedict": wn}, X)
+    # c5 varying white noise: the HD process stacked on sampled efac / equad /
+    # ecorr (enterprise_models.py:108-146 under :390-403): per-sample
+    # contraction, partial factorisation with the timing model in
+    c5v = synth.config_c5(n_psr=4, n_toa=500, seed=57, epoch_size=4, gwb="hd_vary_gamma_5_nfreqs", nfreqs=10,
+                          fixed_white=False)
+    X = np.vstack([synth.prior_draws(c5v.pta, 8, 58), synth.near_draws(c5v.pta, c5v.truth, 8, 59)])
+    dump("c5_varwn", c5v.pta, recipe_of(c5v, c5v.terms, c5v.common, False), X)
+    # c1 wide: the reference's example pulsar with 60 frequencies per term
+    # (X_60_nfreqs, enterprise_models.py:148-167; fake_psr_0's own rule gives
+    # 60) for red, DM and chromatic noise: 376 basis columns, past the register
+    # kernels (chol_wide_kernel / contract_wide_kernel); white noise sampled
+    # (c1_wide) and fixed at the example noise file (c1_widefix)
+    c1w = synth.config_c1(os.path.join(HERE, "ref_examples"))
+    psr = c1w.pta.signal_collections[0].psr
+    terms_w = {"efac": "by_backend", "equad": "by_backend", "spin_noise": "powerlaw_60_nfreqs",
+               "dm_noise": "powerlaw_60_nfreqs", "chromred": "4_60_nfreqs"}
+    for name, fixed in (("c1_wide", False), ("c1_widefix", True)):
+        ns = synth.params_namespace(np.ptp(psr.toas), fixed)
+        wn = {k: v for k, v in c1w.truth.items() if k.endswith("_efac") or k.endswith("_log10_tnequad")}
+        pta_w = synth.build_pta([psr], terms_w, {}, ns, wn if fixed else None)
+        truth_w = synth.truth_values(pta_w, 21, white=wn)
+        synth.simulate_residuals(pta_w, truth_w, 22)
+        X = np.vstack([synth.prior_draws(pta_w, 8, 23), synth.near_draws(pta_w, truth_w, 8, 24)])
+        dump(name, pta_w, {"per_psr_terms": terms_w, "common_terms": {}, "Tspan": float(np.ptp(psr.toas)),
+                           "fixed_white": fixed, "noisedict": wn if fixed else {}}, X)
 
 
 if __name__ == "__main__":

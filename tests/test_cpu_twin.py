@@ -46,8 +46,8 @@ def test_twin_goldens_and_surface(twin_lib):
     print(p.stdout)
     assert res["lib"] == "libewarp_cpu.so"
     assert set(res["goldens"]) == {"c1_j1832", "c1_turnover", "c1_system", "c2_small", "c2_chromvary", "c3_small",
-                                   "c3_freesp", "c4_small"}
-    assert set(res["refused"]) == {"c5_small", "c5_mono", "c5_noauto", "c5_dipo"}
+                                   "c3_freesp", "c4_small", "c1_wide", "c1_widefix"}
+    assert set(res["refused"]) == {"c5_small", "c5_mono", "c5_noauto", "c5_dipo", "c5_varwn"}
     assert all("device-only" in v for v in res["refused"].values())
     assert res["set_fixed_white_equal"] and res["set_fixed_white_changed"]
     assert res["unit_terms_sum_ok"]

@@ -36,3 +36,17 @@ def test_latency_variants_vs_batched(mode):
                        capture_output=True, text=True, timeout=600, env=env)
     print(r.stdout[-4000:], r.stderr[-2000:])
     assert r.returncode == 0
+
+
+def test_latency_stall_is_an_error():
+    """A chol_lat_kernel unit whose LDS-counter wait runs out is an error of
+    ewh_lnl_batch (EWH_E_HIP), not a NaN lnL; forced by dev kernel mode 23
+    (scripts/lat_stall_check.py)."""
+    lib = os.path.join(ROOT, "enterprise_warp_amd", "libewarp_hip_dev.so")
+    if not os.path.exists(lib):
+        pytest.skip("dev library not built (make -C enterprise_warp_amd/csrc dev)")
+    env = dict(os.environ, EWARP_HIP_LIB=lib)
+    r = subprocess.run([sys.executable, os.path.join(ROOT, "scripts", "lat_stall_check.py")],
+                       capture_output=True, text=True, timeout=600, env=env)
+    print(r.stdout[-4000:], r.stderr[-2000:])
+    assert r.returncode == 0

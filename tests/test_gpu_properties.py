@@ -238,3 +238,58 @@ def test_correlated_right_looking_small_chunks(require_gpu):
     for B in (1, 3, 4):
         got = np.concatenate([pta.get_lnlikelihood_batch(X[i:i + B]) for i in range(0, len(X), B)])
         np.testing.assert_array_equal(got, left)
+
+
+@pytest.mark.parametrize("name", ["c4_small", "c3_small", "c2_small", "c5_small", "c5_varwn", "c1_system"])
+def test_wide_kernel_matches_register_kernels(require_gpu, name):
+    """chol_wide_kernel (fp64, any width: the partial factorisation of a wide
+    correlated model, and kernel mode 27's route for every factorisation)
+    against the default kernels on the same inputs: chol_big_kernel (c4_small,
+    13 blocks: the same operations per block in the same order, unit terms
+    equal to ~1 ulp), chol_mfma_kernel (right-looking, one log-determinant
+    accumulator) and its KEEP form, at 1e-3 of strict; c1_system (fixed white
+    noise, 13 blocks; by default the double-double chol_dd_kernel) on its
+    near-truth draws at the strict bound."""
+    from conftest import load_golden
+    pta, z = load_golden(name, full=True)
+    X = z["theta"]
+    eng = pta.engine()
+    eng.set_kernel_mode(2)                           # (the latency path off: batched kernels only)
+    a = pta.get_lnlikelihood_batch(X)
+    ta = eng.unit_terms(len(X))
+    eng.set_kernel_mode(27)
+    try:
+        b = pta.get_lnlikelihood_batch(X)
+        tb = eng.unit_terms(len(X))
+    finally:
+        eng.set_kernel_mode(0)
+    assert np.array_equal(np.isfinite(a), np.isfinite(b)) and not np.any(np.isnan(b))
+    if name == "c1_system":
+        check_parity(b[z["near"]], a[z["near"]], "c1_system wide (fp64) vs dd")
+        return
+    fin = np.isfinite(a)
+    err = np.abs(b[fin] - a[fin]) / (1e-6 + 1e-10 * np.abs(a[fin]))
+    assert err.max() <= 1e-3, f"{name}: wide vs register {err.max():.3e} of strict"
+    if name == "c4_small":
+        tf = np.isfinite(ta)
+        np.testing.assert_allclose(tb[tf], ta[tf], rtol=1e-14, atol=0)
+
+
+def test_wide_bases_full_size(require_gpu):
+    """A basis past every register kernel at a realistic size: one pulsar of
+    10k TOAs with red / DM / chromatic noise at 60 frequencies each (X_60_nfreqs,
+    enterprise_models.py:148-167; 12 + 360 columns, 24 blocks): white noise
+    sampled (contract_wide_kernel + chol_wide_kernel) and fixed (gram_dd +
+    schur + chol_wide_kernel), near-truth draws against the oracle, strict."""
+    from conftest import oracle_lnl
+    psr = synth.make_pulsar("J0000+0060", 10000, seed=60, epoch_size=16)
+    terms = {"efac": "by_backend", "equad": "by_backend", "ecorr": "by_backend",
+             "spin_noise": "powerlaw_60_nfreqs", "dm_noise": "powerlaw_60_nfreqs", "chromred": "4_60_nfreqs"}
+    wn = synth.white_noisedict([psr], 61)
+    for fixed in (False, True):
+        ns = synth.params_namespace(psr.toas.max() - psr.toas.min(), fixed)
+        pta = synth.build_pta([psr], terms, {}, ns, wn if fixed else None)
+        truth = synth.truth_values(pta, 62, white=wn)
+        synth.simulate_residuals(pta, truth, 63)
+        X = synth.near_draws(pta, truth, 6, 64)
+        check_parity(pta.get_lnlikelihood_batch(X), oracle_lnl(pta, X), f"wide 372 columns, fixed white {fixed}")
