@@ -239,18 +239,20 @@ def kernel_sources_sha():
     return hsh.hexdigest()[:16]
 
 
-def sampler_latency(pta, cfg, batches=(1, 16, 256), reps=50):
+def sampler_latency(pta, cfg, batches=(1, 16, 256, 4096), reps=50):
     """The drop-in as samplers call it: host theta in, host lnL out through
     ewh_lnl_batch (pinned staging, H2D, launches, D2H, stream sync), one
     process, C3.  PTMCMC / bilby call one theta at a time
-    (run_example_paramfile.py:27-30, bilby_warp.py:35)."""
+    (run_example_paramfile.py:27-30, bilby_warp.py:35).  B4096 is the
+    headline batch with its host transfers included (the headline `value`
+    keeps theta and lnL resident in HBM)."""
     from enterprise_warp_amd import synth
     out = {}
     for B in batches:
         X = synth.prior_draws(pta, B, 7 + B)
         pta.get_lnlikelihood_batch(X)
         ts = []
-        for _ in range(reps):
+        for _ in range(reps if B < 4096 else 10):
             t0 = time.perf_counter()
             pta.get_lnlikelihood_batch(X)
             ts.append(time.perf_counter() - t0)

@@ -21,7 +21,7 @@ LIB_PATH = os.environ.get("EWARP_HIP_LIB") or (CPU_LIB_PATH if BACKEND == "cpu" 
                                                os.path.join(_HERE, "libewarp_hip.so"))
 DEV_LIB_PATH = os.path.join(_HERE, "libewarp_hip_dev.so")
 
-EWH_ABI_VERSION = 5
+EWH_ABI_VERSION = 6
 COMMON_CORRELATED, COMMON_OPTSTAT = 0, 1
 SPEC_POWERLAW, SPEC_TURNOVER, SPEC_FREESPEC, SPEC_CONST = 1, 2, 3, 4
 
@@ -62,6 +62,7 @@ class PtaDesc(C.Structure):
 EXPORTS = ["ewh_create", "ewh_num_devices", "ewh_set_fixed_white", "ewh_lnl_batch", "ewh_lnl_units_device",
            "ewh_keep_dim", "ewh_corr_partial_device", "ewh_corr_finish_device",
            "ewh_last_unit_terms", "ewh_unit_cost", "ewh_set_kernel_mode", "ewh_optstat", "ewh_contract_device",
+           "ewh_transfer_stats",
            "ewh_destroy", "ewh_last_error", "ewh_version"]
 DEV_EXPORTS = ["ewh_dev_gram", "ewh_dev_reduced"]
 
@@ -119,6 +120,8 @@ def load():
     lib.ewh_optstat.restype = C.c_int
     lib.ewh_contract_device.argtypes = [C.c_void_p, C.c_void_p, C.c_int32, C.c_void_p]
     lib.ewh_contract_device.restype = C.c_int
+    lib.ewh_transfer_stats.argtypes = [C.c_void_p, C.POINTER(C.c_int64), C.POINTER(C.c_int64)]
+    lib.ewh_transfer_stats.restype = C.c_int
     lib.ewh_destroy.argtypes = [C.c_void_p]
     lib.ewh_destroy.restype = None
     lib.ewh_last_error.argtypes = []

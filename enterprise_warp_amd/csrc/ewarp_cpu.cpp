@@ -361,6 +361,13 @@ int ewh_last_unit_terms(ewh_handle* H, double* out, int32_t B) {
   return 0;
 }
 
+int ewh_transfer_stats(const ewh_handle* H, int64_t* h2d_bytes, int64_t* peer) {
+  if (!H) return set_err(EWH_E_INVALID, "bad handle");
+  if (h2d_bytes) *h2d_bytes = 0;     // host twin: nothing crosses a bus
+  if (peer) *peer = 1;
+  return 0;
+}
+
 double ewh_unit_cost(const ewh_handle* H, int32_t p) {
   if (!H || p < 0 || p >= (int)H->psr.size()) return 0.0;
   const Psr& P = H->psr[p];

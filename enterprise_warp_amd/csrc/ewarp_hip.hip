@@ -879,25 +879,32 @@ void dchol_rowupdate2_kernel(double* __restrict__ mats, int Np, int i) {
 // U_pk is staged through LDS (shared by the four waves), each wave's U_pj
 // slab comes from global memory into registers.  Same sums, same order as
 // dchol_rowupdate2_kernel + dchol_panel_reg_kernel: bit-identical.
-__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(3, 3)))
+// TPW = 2 (dev A/B, kernel mode 28): two tiles (k, j), (k, j + 1) per
+// 8-wave workgroup sharing one LDS copy of U_pk -- per p the workgroup reads
+// 96 KB (U_pk + two U_pj) for two tiles instead of 64 KB for one.
+template <int TPW>
+__global__ __launch_bounds__(256 * TPW) __attribute__((amdgpu_waves_per_eu(TPW == 1 ? 3 : 4, TPW == 1 ? 3 : 4)))
 void dchol_rowpanel_kernel(double* __restrict__ mats, int Np, int k, const double* __restrict__ wbuf) {
+  constexpr int NT = 256 * TPW, RW = 64 / (NT / 64);   // threads; U_pk rows staged per thread
   __shared__ double Uk[DCB][DCB + 1];
-  const int j = k + 1 + blockIdx.x, bl = blockIdx.y, t = threadIdx.x;
+  const int t = threadIdx.x, wave = t >> 6, tile = wave >> 2, w = wave & 3;
+  const int j = k + 1 + TPW * blockIdx.x + tile, bl = blockIdx.y;
+  const bool live = j < Np / DCB;                  // (the last workgroup of an odd row: one tile)
   double* base = mats + (long long)bl * Np * Np;
-  double* Akj = base + (long long)(DCB * k) * Np + DCB * j;
-  const int w = t >> 6, lane = t & 63, q = lane >> 4, c = lane & 15;
+  double* Akj = base + (long long)(DCB * k) * Np + DCB * (live ? j : k + 1);
+  const int lane = t & 63, q = lane >> 4, c = lane & 15;
   v4d acc[4];
 #pragma unroll
   for (int s0 = 0; s0 < 4; ++s0)
 #pragma unroll
-    for (int r = 0; r < 4; ++r) acc[s0][r] = Akj[(long long)(16 * s0 + q + 4 * r) * Np + 16 * w + c];
-  const double* bcol = base + DCB * j + 16 * w + c + (long long)q * Np;
+    for (int r = 0; r < 4; ++r) acc[s0][r] = live ? Akj[(long long)(16 * s0 + q + 4 * r) * Np + 16 * w + c] : 0.0;
+  const double* bcol = base + DCB * (live ? j : k + 1) + 16 * w + c + (long long)q * Np;
   const double* acol = base + DCB * k + (t & 63) + (long long)(t >> 6) * Np;
-  double pa[16];
+  double pa[RW];
   auto aload = [&](int p) {
     const double* rp = acol + (long long)(DCB * p) * Np;
 #pragma unroll
-    for (int r = 0; r < 16; ++r) pa[r] = rp[(long long)(4 * r) * Np];
+    for (int r = 0; r < RW; ++r) pa[r] = rp[(long long)((NT / 64) * r) * Np];
   };
   if (k > 0) aload(0);
   for (int p = 0; p < k; ++p) {
@@ -907,7 +914,7 @@ void dchol_rowpanel_kernel(double* __restrict__ mats, int Np, int k, const doubl
     for (int ts = 0; ts < 16; ++ts) b[ts] = bp[(long long)(4 * ts) * Np];
     __syncthreads();
 #pragma unroll
-    for (int r = 0; r < 16; ++r) Uk[(t >> 6) + 4 * r][t & 63] = pa[r];
+    for (int r = 0; r < RW; ++r) Uk[(t >> 6) + (NT / 64) * r][t & 63] = pa[r];
     __syncthreads();
     if (p + 1 < k) aload(p + 1);
 #pragma unroll
@@ -917,6 +924,7 @@ void dchol_rowpanel_kernel(double* __restrict__ mats, int Np, int k, const doubl
         acc[s0] = __builtin_amdgcn_mfma_f64_16x16x4f64(Uk[4 * ts + q][16 * s0 + c], b[ts], acc[s0], 0, 0, 1);
     }
   }
+  if (!live) return;
   // the panel: U_kj = L_kk^-1 A_kj on this strip (dchol_panel_reg_kernel)
   const double* W = wbuf + (long long)bl * DW_SLOTS * 256 + lane * 4;
   static_for<0, 4>([&](auto SS) {
@@ -1067,6 +1075,24 @@ __global__ void reduce_units_kernel(const double* __restrict__ units, int P, int
   out[b] = s;
 }
 
+// Multi-context handle, theta staging: segment s of the table (5 ints: row_lo,
+// row_hi, ncol, column-list offset, payload offset; the column lists follow
+// the nseg records) scatters its packed rows x columns payload into the
+// full-layout theta [B x np] of this device.  Columns and rows outside the
+// segments are never read by the context's units.
+__global__ __launch_bounds__(256) void expand_theta_kernel(const double* __restrict__ stage,
+                                                           const int* __restrict__ seg, int nseg, int np,
+                                                           double* __restrict__ theta) {
+  const int* rec = seg + 5 * blockIdx.x;
+  const int r0 = rec[0], nr = rec[1] - rec[0], nc = rec[2];
+  const int* cols = seg + 5 * nseg + rec[3];
+  const double* src = stage + rec[4];
+  for (int idx = threadIdx.x; idx < nr * nc; idx += 256) {
+    const int r = idx / nc, j = idx - r * nc;
+    theta[(long long)(r0 + r) * np + cols[j]] = src[idx];
+  }
+}
+
 // Multi-context handle: out[b] = sum_i part[i * B + b], the contexts' partial
 // sums (each over its unit range, pulsars in order) in context order.
 __global__ void fold_partials_kernel(const double* __restrict__ part, int nd, int B, double* __restrict__ out) {
@@ -1180,6 +1206,17 @@ struct DevCtx {
   // latency path of small single-device batches (chol_lat.hip): every pulsar
   // has the same reduced block count lat_nb <= LAT_NB_MAX (0: not eligible)
   int lat_nb = 0;
+  // multi-context batches: the theta entries this context's units read,
+  // packed in pinned host memory (h_stage), copied to d_stage and scattered
+  // into d_theta by expand_theta_kernel along the segment table d_seg
+  double* h_stage = nullptr;
+  size_t h_stage_cap = 0;
+  int* h_seg = nullptr;
+  size_t h_seg_cap = 0;
+  double* d_stage = nullptr;
+  size_t d_stage_cap = 0;
+  int* d_seg = nullptr;
+  size_t d_seg_cap = 0;
 };
 
 namespace {
@@ -1835,7 +1872,14 @@ int corr_finish(DevCtx* h, const double* theta_dev, int B, const double* keep, d
           hipLaunchKernelGGL(HIP_KERNEL_NAME(dchol_diag_reg_kernel<true>), dim3(nb), dim3(64), 0, st, h->d_dense,
                              h->Np, k, h->d_wbuf, h->d_cldet, h->d_cq, h->d_cfail);
         if (m > 0 && fused)
-          hipLaunchKernelGGL(dchol_rowpanel_kernel, dim3(m, nb), dim3(256), 0, st, h->d_dense, h->Np, k, h->d_wbuf);
+        {
+          if (h->kernel_mode == 28)   // (dev A/B: two tiles per workgroup)
+            hipLaunchKernelGGL(HIP_KERNEL_NAME(dchol_rowpanel_kernel<2>), dim3((m + 1) / 2, nb), dim3(512), 0, st,
+                               h->d_dense, h->Np, k, h->d_wbuf);
+          else
+            hipLaunchKernelGGL(HIP_KERNEL_NAME(dchol_rowpanel_kernel<1>), dim3(m, nb), dim3(256), 0, st, h->d_dense,
+                               h->Np, k, h->d_wbuf);
+        }
         else if (m > 0)
           hipLaunchKernelGGL(dchol_panel_reg_kernel, dim3(4 * m, nb), dim3(64), 0, st, h->d_dense, h->Np, k,
                              h->d_wbuf);
@@ -1867,6 +1911,8 @@ void destroy_ctx(DevCtx* h) {
   (void)hipSetDevice(h->device);
   if (h->stream) (void)hipStreamSynchronize(h->stream);
   drop_graphs(h);
+  if (h->h_stage) (void)hipHostFree(h->h_stage);
+  if (h->h_seg) (void)hipHostFree(h->h_seg);
   for (void* p : h->allocs) (void)hipFree(p);
   if (h->stream) (void)hipStreamDestroy(h->stream);
   delete h;
@@ -2382,6 +2428,13 @@ struct ewh_handle {
   // latency path: device addresses of h_theta / h_out (for the host pointers recorded)
   const double *lat_th_host = nullptr, *lat_out_host = nullptr;
   double *lat_th_dev = nullptr, *lat_out_dev = nullptr;
+  // theta columns each pulsar's units read (white-noise slots, spectra,
+  // chromatic index groups; a correlated process's common spectra)
+  std::vector<std::vector<int>> psr_cols;
+  // ewh_transfer_stats: theta bytes host -> device of the last batch, and the
+  // contexts with peer access to the first one
+  long long h2d_bytes = 0;
+  long long peer_mask = 1;
 };
 
 namespace {
@@ -2422,6 +2475,91 @@ int enqueue_single(ewh_handle* H, DevCtx* h, int B) {
 
 constexpr size_t GRAPH_CACHE = 8;
 
+template <typename T>
+int ensure_host_pinned(T** p, size_t* cap, size_t need) {
+  if (need <= *cap) return 0;
+  if (*p) (void)hipHostFree(*p);
+  *p = nullptr;
+  *cap = 0;
+  hipError_t e = hipHostMalloc((void**)p, std::max<size_t>(need, 1) * sizeof(T), hipHostMallocPortable);
+  if (e != hipSuccess) return set_err(EWH_E_NOMEM, std::string("hipHostMalloc: ") + hipGetErrorString(e));
+  *cap = need;
+  return 0;
+}
+
+template <typename T>
+int ensure_dev(DevCtx* h, T** p, size_t* cap, size_t need) {
+  if (need <= *cap) return 0;
+  if (*p) {
+    (void)hipFree(*p);
+    h->allocs.erase(std::find(h->allocs.begin(), h->allocs.end(), (void*)*p));
+    *p = nullptr;
+  }
+  *cap = 0;
+  int rc = dalloc(h, p, need);
+  if (rc) return rc;
+  *cap = need;
+  return 0;
+}
+
+// Theta of one context's unit range [a, b) (u = pulsar * B + sample): per
+// column, the sample rows its pulsars read (the union of their row ranges);
+// columns with the same rows form one segment.  Packed into pinned memory,
+// copied to the device and scattered into h->d_theta (full layout) on
+// h->stream.  Returns the payload bytes (or a negative error code).
+long long stage_theta_range(ewh_handle* H, DevCtx* h, const double* theta_host, int B, long long a, long long b) {
+  const int np = H->n_param;
+  if (b <= a || np <= 0) return 0;
+  std::map<int, std::pair<int, int>> rows;                 // column -> [lo, hi)
+  const int p0 = (int)(a / B), p1 = (int)((b - 1) / B);
+  for (int p = p0; p <= p1; ++p) {
+    const int lo = p == p0 ? (int)(a % B) : 0, hi = p == p1 ? (int)((b - 1) % B) + 1 : B;
+    for (int c : H->psr_cols[p]) {
+      auto it = rows.find(c);
+      if (it == rows.end()) rows.emplace(c, std::make_pair(lo, hi));
+      else it->second = {std::min(it->second.first, lo), std::max(it->second.second, hi)};
+    }
+  }
+  std::map<std::pair<int, int>, std::vector<int>> segs;
+  for (auto& kv : rows) segs[kv.second].push_back(kv.first);
+  const int nseg = (int)segs.size();
+  if (nseg == 0) return 0;
+  size_t ncolsum = 0, payload = 0;
+  for (auto& kv : segs) {
+    ncolsum += kv.second.size();
+    payload += (size_t)(kv.first.second - kv.first.first) * kv.second.size();
+  }
+  int rc;
+  if ((rc = ensure_host_pinned(&h->h_stage, &h->h_stage_cap, payload)) ||
+      (rc = ensure_host_pinned(&h->h_seg, &h->h_seg_cap, 5 * (size_t)nseg + ncolsum)) ||
+      (rc = ensure_dev(h, &h->d_stage, &h->d_stage_cap, payload)) ||
+      (rc = ensure_dev(h, &h->d_seg, &h->d_seg_cap, 5 * (size_t)nseg + ncolsum)))
+    return rc;
+  int si = 0, coloff = 0;
+  size_t dataoff = 0;
+  for (auto& kv : segs) {
+    const int lo = kv.first.first, hi = kv.first.second, nc = (int)kv.second.size();
+    int* rec = h->h_seg + 5 * si;
+    rec[0] = lo; rec[1] = hi; rec[2] = nc; rec[3] = coloff; rec[4] = (int)dataoff;
+    for (int j = 0; j < nc; ++j) h->h_seg[5 * nseg + coloff + j] = kv.second[j];
+    for (int r = lo; r < hi; ++r) {
+      const double* src = theta_host + (size_t)r * np;
+      double* dst = h->h_stage + dataoff + (size_t)(r - lo) * nc;
+      for (int j = 0; j < nc; ++j) dst[j] = src[kv.second[j]];
+    }
+    dataoff += (size_t)(hi - lo) * nc;
+    coloff += nc;
+    ++si;
+  }
+  EWH_HIP(hipMemcpyAsync(h->d_seg, h->h_seg, sizeof(int) * (5 * (size_t)nseg + ncolsum), hipMemcpyHostToDevice,
+                         h->stream));
+  EWH_HIP(hipMemcpyAsync(h->d_stage, h->h_stage, sizeof(double) * payload, hipMemcpyHostToDevice, h->stream));
+  hipLaunchKernelGGL(expand_theta_kernel, dim3(nseg), dim3(256), 0, h->stream, h->d_stage, h->d_seg, nseg, np,
+                     h->d_theta);
+  EWH_HIP(hipGetLastError());
+  return (long long)(payload * sizeof(double));
+}
+
 // Correlated common process, batch smaller than the device count (one
 // PTMCMC proposal): the pulsars are split over the devices (the exchange step
 // of SURVEY.md §8(e)) -- each device runs the partial factorisations of its
@@ -2447,15 +2585,18 @@ int lnl_batch_corr_pulsars(ewh_handle* H, int B, double* out_host) {
   if (np > 0)
     EWH_HIP(hipMemcpyAsync(h0->d_theta, H->h_theta, sizeof(double) * (size_t)B * np, hipMemcpyHostToDevice,
                            h0->stream));
+  H->h2d_bytes += (long long)sizeof(double) * B * np;
   EWH_HIP(hipStreamSynchronize(h0->stream));
   for (int i = 0; i < nd; ++i) {
     DevCtx* h = H->ctx[i];
     const int p0 = (int)((long long)P * i / nd), p1 = (int)((long long)P * (i + 1) / nd);
     if (p1 <= p0) continue;
     EWH_HIP(hipSetDevice(h->device));
-    if (np > 0 && i > 0)
+    if (np > 0 && i > 0) {
       EWH_HIP(hipMemcpyAsync(h->d_theta, H->h_theta, sizeof(double) * (size_t)B * np, hipMemcpyHostToDevice,
                              h->stream));
+      H->h2d_bytes += (long long)sizeof(double) * B * np;
+    }
     if ((rc = corr_partial(h, h->d_theta, B, p0, p1, h->d_units, h->d_keep, h->stream))) return rc;
     if (i > 0) {   // gather: this device's pulsar slices into the first device
       EWH_HIP(hipMemcpyPeerAsync(h0->d_keep + (size_t)p0 * B * kd2, h0->device, h->d_keep + (size_t)p0 * B * kd2,
@@ -2624,6 +2765,29 @@ int ewh_create(const ewh_pta_desc* d, const int32_t* device_ids, int32_t ndev, e
   ewh_handle* H = new ewh_handle();
   H->P = d->n_pulsar;
   H->n_param = d->n_param;
+  H->psr_cols.resize(d->n_pulsar);
+  for (int p = 0; p < d->n_pulsar; ++p) {
+    const ewh_pulsar_desc& sd = d->pulsars[p];
+    std::vector<int>& cols = H->psr_cols[p];
+    auto add = [&](const ewh_pref& r) {
+      if (r.idx >= 0) cols.push_back(r.idx);
+    };
+    for (int i = 0; i < sd.n_slot; ++i) add(sd.slots[i]);
+    for (int e = 0; e < sd.n_spec; ++e) {
+      add(sd.spec[e].p0);
+      add(sd.spec[e].p1);
+      add(sd.spec[e].p2);
+    }
+    for (int g = 0; g < sd.n_bgroup; ++g) add(sd.bgroup_idx[g]);
+    if (d->common && d->common->spec)
+      for (int g = 0; g < d->common->n_col; ++g) {
+        add(d->common->spec[g].p0);
+        add(d->common->spec[g].p1);
+        add(d->common->spec[g].p2);
+      }
+    std::sort(cols.begin(), cols.end());
+    cols.erase(std::unique(cols.begin(), cols.end()), cols.end());
+  }
   std::vector<ProjCoef> proj(d->n_pulsar);
   for (int p = 0; p < d->n_pulsar; ++p) proj[p] = projection_coef(d->pulsars[p]);
   for (int id : ids) {
@@ -2635,7 +2799,35 @@ int ewh_create(const ewh_pta_desc* d, const int32_t* device_ids, int32_t ndev, e
     H->ctx.push_back(c);
   }
   H->corr = H->ctx[0]->corr;
+  // peer access between every context's device and the first one (both
+  // directions: partial B-vectors and gathered kept blocks move device to
+  // device); bit i of peer_mask records context i
+  H->peer_mask = 1;
+  for (size_t i = 1; i < ids.size(); ++i) {
+    bool ok = ids[i] == ids[0];
+    if (!ok) {
+      int a = 0, b = 0;
+      if (hipDeviceCanAccessPeer(&a, ids[i], ids[0]) == hipSuccess && hipDeviceCanAccessPeer(&b, ids[0], ids[i]) ==
+                                                                             hipSuccess && a && b) {
+        hipError_t e1 = hipSetDevice(ids[i]);
+        if (e1 == hipSuccess) e1 = hipDeviceEnablePeerAccess(ids[0], 0);
+        hipError_t e2 = hipSetDevice(ids[0]);
+        if (e2 == hipSuccess) e2 = hipDeviceEnablePeerAccess(ids[i], 0);
+        ok = (e1 == hipSuccess || e1 == hipErrorPeerAccessAlreadyEnabled) &&
+             (e2 == hipSuccess || e2 == hipErrorPeerAccessAlreadyEnabled);
+        (void)hipGetLastError();
+      }
+    }
+    if (ok) H->peer_mask |= 1LL << i;
+  }
   *out = H;
+  return 0;
+}
+
+int ewh_transfer_stats(const ewh_handle* H, int64_t* h2d_bytes, int64_t* peer) {
+  if (!H) return set_err(EWH_E_INVALID, "bad handle");
+  if (h2d_bytes) *h2d_bytes = H->h2d_bytes;
+  if (peer) *peer = H->peer_mask;
   return 0;
 }
 
@@ -2707,9 +2899,18 @@ int ewh_lnl_batch(ewh_handle* H, const double* theta_host, int32_t B, double* ou
   if (H->ctx[0]->osmode) return set_err(EWH_E_UNSUPPORTED, "an optimal-statistic handle evaluates ewh_optstat only");
   const int nd = (int)H->ctx.size(), np = H->n_param;
   int rc;
-  if ((rc = ensure_pinned(&H->h_theta, &H->h_theta_cap, (size_t)B * std::max(1, np), &H->lat_th_host))) return rc;
-  if (np > 0) std::memcpy(H->h_theta, theta_host, sizeof(double) * (size_t)B * np);
-  if (nd == 1) return lnl_batch_single(H, H->ctx[0], B, out_host);
+  H->h2d_bytes = 0;
+  if (nd == 1 || H->corr) {
+    // (single context: the batch's theta rows, read by the latency kernel
+    // straight from the pinned staging or copied once; correlated: each
+    // context's sample slice, or every pulsar partition its copy)
+    if ((rc = ensure_pinned(&H->h_theta, &H->h_theta_cap, (size_t)B * std::max(1, np), &H->lat_th_host))) return rc;
+    if (np > 0) std::memcpy(H->h_theta, theta_host, sizeof(double) * (size_t)B * np);
+  }
+  if (nd == 1) {
+    H->h2d_bytes = (long long)sizeof(double) * B * np;
+    return lnl_batch_single(H, H->ctx[0], B, out_host);
+  }
   if (H->corr && B < nd) return lnl_batch_corr_pulsars(H, B, out_host);
   std::vector<std::pair<long long, long long>> split;
   if (H->corr) {
@@ -2755,6 +2956,7 @@ int ewh_lnl_batch(ewh_handle* H, const double* theta_host, int32_t B, double* ou
       if (np > 0)
         EWH_HIP(hipMemcpyAsync(h->d_theta, H->h_theta + (size_t)a * np, sizeof(double) * (size_t)Bd * np,
                                hipMemcpyHostToDevice, h->stream));
+      H->h2d_bytes += (long long)sizeof(double) * Bd * np;
       if ((rc = ctx_units(h, h->d_theta, Bd, 0, (long long)H->P * Bd, h->d_out, h->stream, true))) return rc;
       EWH_HIP(hipMemcpyAsync(H->h_out + a, h->d_out, sizeof(double) * Bd, hipMemcpyDeviceToHost, h->stream));
     } else {
@@ -2762,9 +2964,11 @@ int ewh_lnl_batch(ewh_handle* H, const double* theta_host, int32_t B, double* ou
       // (rows outside the range are zero) into a B-vector, which goes to the
       // first device; only B doubles ever come back to the host
       if ((rc = ensure_io(h, B))) return rc;
-      if (b > a && np > 0)
-        EWH_HIP(hipMemcpyAsync(h->d_theta, H->h_theta, sizeof(double) * (size_t)B * np, hipMemcpyHostToDevice,
-                               h->stream));
+      // only the theta entries this context's units read (the host packs
+      // context i + 1's while context i's copy and launches run)
+      const long long nbytes = stage_theta_range(H, h, theta_host, B, a, b);
+      if (nbytes < 0) return (int)nbytes;
+      H->h2d_bytes += nbytes;
       if ((rc = ctx_units(h, h->d_theta, B, a, b, h->d_out, h->stream, true))) return rc;
       EWH_HIP(hipMemcpyPeerAsync(H->d_part + (size_t)i * B, h0->device, h->d_out, h->device, sizeof(double) * B,
                                  h->stream));

@@ -502,6 +502,13 @@ class Engine:
         _lib.check(self.lib.ewh_last_unit_terms(self.h, _as_ptr(out, C.c_double), int(B)))
         return out
 
+    def transfer_stats(self):
+        """(theta bytes host -> device of the last batch, peer-access mask of
+        the contexts) -- ewh_transfer_stats."""
+        b, m = C.c_int64(), C.c_int64()
+        _lib.check(self.lib.ewh_transfer_stats(self.h, C.byref(b), C.byref(m)))
+        return int(b.value), int(m.value)
+
     def unit_costs(self):
         return np.array([self.lib.ewh_unit_cost(self.h, p) for p in range(self.n_pulsar)])
 

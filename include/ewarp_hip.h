@@ -54,7 +54,7 @@
 extern "C" {
 #endif
 
-#define EWH_ABI_VERSION 5
+#define EWH_ABI_VERSION 6
 
 enum ewh_status {
   EWH_OK = 0,
@@ -182,7 +182,8 @@ int ewh_set_fixed_white(ewh_handle* h, const double* values);
 /* lnL for B samples: theta_host [B x n_param], out_host [B]. Synchronous.
  * Several devices: uncorrelated / CURN models split the (pulsar, sample)
  * units into cost-balanced contiguous ranges (one per device); each device
- * sums its range over its pulsars (pulsar order) into a B-vector, the
+ * receives only the theta entries its range reads and sums its range over
+ * its pulsars (pulsar order) into a B-vector, the
  * B-vectors are peer-copied to the first device and added there in device
  * order, and only B doubles return to the host (equal to one device at the
  * strict bound, not bit for bit: the fold is re-associated).  A correlated
@@ -250,6 +251,15 @@ int ewh_last_unit_terms(ewh_handle* h, double* out_host, int32_t B);
 /* Cost model used for sharding: relative cost of one unit of pulsar p. */
 double ewh_unit_cost(const ewh_handle* h, int32_t pulsar);
 
+/* Transfers of the last ewh_lnl_batch: *h2d_bytes = theta bytes copied host
+ * -> device over all contexts (each context receives only the theta entries
+ * its units read: per column, the sample rows of its unit range); *peer =
+ * bit i set when context i > 0 has peer access to the first context's device
+ * (enabled in ewh_create where the devices allow it; the partial B-vectors
+ * and gathered blocks then move device to device) -- context 0 and contexts
+ * on the first device set their bit too.  Either pointer may be NULL. */
+int ewh_transfer_stats(const ewh_handle* h, int64_t* h2d_bytes, int64_t* peer);
+
 /* Kernel selection: 0 = auto (register-blocked MFMA factorisation with the
  * two-level LDL^T panel -- the 16x16 diagonal block in 4-row sub-panels by
  * VALU, each closed by one symmetric MFMA rank-4 update, the rest of the
@@ -261,7 +271,9 @@ double ewh_unit_cost(const ewh_handle* h, int32_t pulsar);
  * that latency path (batched kernels at every batch size), 1 = force the
  * LDS kernel (unblocked Cholesky; for a
  * correlated common process also the round-1 dense LDS diagonal-block and
- * panel kernels), 7 = default factorisation with the round-1 kernels
+ * panel kernels), 27 = every factorisation (full and partial) by the fp64
+ * any-width chol_wide_kernel (cross-check of the register, big and
+ * double-double kernels), 7 = default factorisation with the round-1 kernels
  * elsewhere: the contraction (varying white noise: separate epoch-sum
  * kernel, unpipelined tiles) instead of the pipelined one and, for a
  * correlated common process, the right-looking dense update and the LDS
@@ -271,9 +283,11 @@ double ewh_unit_cost(const ewh_handle* h, int32_t pulsar);
  * columns, else 4), 17 = the round-2 one-level panel (NB = 8), 19 = the default with the spectra read through the CSR tables
  * instead of the staged records, 21 = the default with in-kernel phase
  * stamps (NB = 8, ewh_dev_stamps), 22 = the latency kernel with phase
- * stamps (ewh_dev_lat_stamps), 24 / 25 = the latency kernel with block
- * barriers instead of the dataflow panel loop / as in round 3.  Other modes
- * return EWH_E_UNSUPPORTED. */
+ * stamps (ewh_dev_lat_stamps), 23 = the latency kernel with every wait
+ * forced to run out (the stall error path), 24 / 25 = the latency kernel with
+ * block barriers instead of the dataflow panel loop / as in round 3, 26 = the
+ * C3 kernel at one wave per SIMD with the whole triangle resident.  Other
+ * modes return EWH_E_UNSUPPORTED. */
 int ewh_set_kernel_mode(ewh_handle* h, int32_t mode);
 
 void ewh_destroy(ewh_handle* h);

@@ -23,6 +23,12 @@ pmc() {  # pmc <name> <script args> -- counters...
   local sargs=$1; shift
   run pmc_$name 180 rocprofv3 --pmc "$@" --kernel-trace -d gpurun_out/pmc_${TAG}_$name -o run --output-format csv -- python $sargs
 }
+# the PMC passes run scripts/chol_ab.py, which loads the dev library: build
+# (or confirm up to date) both libraries first, so a stale or missing dev
+# build stops the profile here instead of after the bench
+run make 600 make -C enterprise_warp_amd/csrc -j16 all dev
+test -f enterprise_warp_amd/libewarp_hip_dev.so || { echo "dev library missing: stopping"; exit 1; }
+python -c "import bench; print('kernel sources sha', bench.kernel_sources_sha())" > gpurun_out/kernel_sources_sha_$TAG.txt
 run bench 400 python bench.py --steps 20 --warmup 3 --cpu-seconds 10
 run rocprof 300 rocprofv3 --kernel-trace --stats -d gpurun_out/prof_$TAG -o run --output-format csv -- python bench.py --steps 20 --warmup 3 --no-cpu-baseline --no-latency
 run configs 400 rocprofv3 --kernel-trace --stats -d gpurun_out/profcfg_$TAG -o run --output-format csv -- python scripts/bench_configs.py --configs c2,c3,c4 --reps 3 --check 3

@@ -105,6 +105,31 @@ def test_multi_context_handle(require_gpu, name):
     pta.engine(devices=[0])
 
 
+def test_multi_context_theta_staging(require_gpu):
+    """A handle spanning a node's contexts sends each context only the theta
+    entries its units read (ewh_transfer_stats): C3's model on 16 pulsars over
+    8 contexts -- the per-pulsar columns once in total, the shared CURN
+    columns once per context -- at most 1.2 x B x n_param x 8 bytes per
+    batch, with the per-pulsar terms bit-identical to one context and peer
+    access recorded for every context."""
+    c3s = synth.config_c3(n_psr=16, n_min=600, n_max=2400, epoch_size=8)
+    pta = c3s.pta
+    B = 256
+    X = synth.prior_draws(pta, B, 77)
+    one = pta.get_lnlikelihood_batch(X)
+    terms1 = pta.engine().unit_terms(B)
+    full = B * len(pta.param_names) * 8
+    eng = pta.engine(devices=[0] * 8)
+    got = pta.get_lnlikelihood_batch(X)
+    nbytes, peer = eng.transfer_stats()
+    print(f"theta bytes {nbytes} = {nbytes / full:.3f} x full, peer mask {peer:#x}")
+    assert nbytes <= 1.2 * full
+    assert peer == 0xff
+    check_parity(got, one, "C3-16psr on 8 contexts")
+    np.testing.assert_array_equal(eng.unit_terms(B), terms1)
+    pta.engine(devices=[0])
+
+
 def test_set_fixed_white_in_place(require_gpu):
     """pta.set_default_params(new white-noise constants) (enterprise_warp.py:
     504-508) updates the cached TNT in place (ewh_set_fixed_white, same
