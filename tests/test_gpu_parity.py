@@ -263,3 +263,47 @@ def test_latency_path_vs_oracle(require_gpu, name):
     near = z["near"]
     check_parity(got[near], oracle_lnl(pta, z["theta"][near]), f"{name}, one theta per call")
     check_accuracy(got, z["lnl"], z["lnl_exact"], f"{name} one theta per call", near=near, per_sample=True)
+
+
+@pytest.mark.parametrize("fixed_white", [True, False])
+def test_correlated_wide_partial_vs_oracle(require_gpu, fixed_white):
+    """A Hellings-Downs process on a basis past the partial register kernel
+    (red, DM and chromatic noise at 30 frequencies each + 14 common
+    frequencies: 188 reduced columns, 12 blocks -> chol_wide_kernel's KEEP
+    form), white noise fixed (the cached double-double S) and sampled
+    (per-sample contraction, block-aligned layout): near-truth draws against
+    the enterprise-order oracle at the strict bound (enterprise_models.py:
+    390-403 stacked on :108-146 and :213-254)."""
+    import numpy as np
+    base = synth.config_c5(n_psr=4, n_toa=600, seed=71, epoch_size=8, gwb="hd_vary_gamma_14_nfreqs", nfreqs=30)
+    psrs = [c.psr for c in base.pta.signal_collections]
+    Tspan = max(p.toas.max() for p in psrs) - min(p.toas.min() for p in psrs)
+    wn = synth.white_noisedict(psrs, 73)
+    terms = dict(base.terms, chromred="4_30_nfreqs")
+    pta = synth.build_pta(psrs, terms, base.common, synth.params_namespace(Tspan, fixed_white),
+                          wn if fixed_white else None)
+    assert max(c.T.shape[1] for c in pta.signal_collections) >= 190
+    truth = synth.truth_values(pta, 74, white=wn)
+    synth.simulate_residuals(pta, truth, 75)
+    X = synth.near_draws(pta, truth, 6, 76)
+    got = pta.get_lnlikelihood_batch(X)
+    assert np.all(np.isfinite(got))
+    check_parity(got, oracle_lnl(pta, X), f"HD wide partial, fixed white {fixed_white}")
+
+
+def test_ptmcmc_fixed_white_latency_path(require_gpu, tmp_path):
+    """PTMCMC (model_utils.setup_sampler, run_example_paramfile.py:25-30) on a
+    fixed-white-noise CURN model: every proposal is one single-theta
+    pta.get_lnlikelihood call, i.e. the latency kernel (chol_lat_kernel).
+    The ln likelihood the chain logged for its last states is re-evaluated
+    by the enterprise-order oracle at the strict bound."""
+    from enterprise_warp_amd import model_utils
+    pta, z = load_golden("c3_small", full=True)
+    s = model_utils.setup_sampler(pta, outdir=str(tmp_path), seed=4)
+    x0 = z["theta"][8]                                  # a near-truth start
+    s.sample(x0, 600, burn=100, thin=10, isave=200, covUpdate=200)
+    ch = np.loadtxt(tmp_path / "chain_1.txt")
+    rows = ch[-8:]
+    npar = len(pta.param_names)
+    want = oracle_lnl(pta, rows[:, :npar])
+    check_parity(rows[:, npar + 1], want, "PTMCMC on c3_small (latency kernel) logged lnL")
