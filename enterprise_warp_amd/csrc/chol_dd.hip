@@ -34,14 +34,15 @@ __device__ __forceinline__ dd dd_sub_mul(dd a, dd x, dd y) {   // a - x y
   return dd_fast(s.hi, s.lo + a.lo - pe);
 }
 
-__global__ __launch_bounds__(256) void chol_dd_kernel(const CholJob* __restrict__ jobs, int B, long long u0, int b_off,
-                                                      const double* __restrict__ theta, int ldth,
-                                                      double* __restrict__ out_units, double* __restrict__ scratch,
-                                                      long long scr_per_wg) {
+// list != NULL: the units are list[0 .. *count) (absolute unit indices, the
+// verify step's flags); the grid loops over them (a workgroup exits at once
+// when there are none).  list == NULL: units u0 + blockIdx.x.
+__device__ void chol_dd_unit(const CholJob* __restrict__ jobs, int B, long long u, int b_off,
+                             const double* __restrict__ theta, int ldth, double* __restrict__ out_units,
+                             double* __restrict__ scratch, long long scr_per_wg) {
   __shared__ double rh[WIDE_LD_MAX], rl[WIDE_LD_MAX], wh[WIDE_LD_MAX], wl[WIDE_LD_MAX];
   __shared__ double red[4];
   const int tid = threadIdx.x, wave = tid >> 6, lane = tid & 63;
-  const long long u = u0 + blockIdx.x;
   const int p = (int)(u / B), b = (int)(u % B);
   const CholJob J = jobs[p];
   const int n = J.ld;
@@ -105,9 +106,48 @@ __global__ __launch_bounds__(256) void chol_dd_kernel(const CholJob* __restrict_
     if (!ok || J.fail) lnl = -INFINITY;
     out_units[(long long)p * B + b] = lnl;
   }
+  __syncthreads();                         // (the workgroup's next unit reuses LDS and scratch)
+}
+
+__global__ __launch_bounds__(256) void chol_dd_kernel(const CholJob* __restrict__ jobs, int B, long long u0, int b_off,
+                                                      const double* __restrict__ theta, int ldth,
+                                                      double* __restrict__ out_units, double* __restrict__ scratch,
+                                                      long long scr_per_wg, const int* __restrict__ list,
+                                                      const int* __restrict__ count) {
+  if (!list) {
+    chol_dd_unit(jobs, B, u0 + blockIdx.x, b_off, theta, ldth, out_units, scratch, scr_per_wg);
+    return;
+  }
+  const int n = *count;
+  for (int i = blockIdx.x; i < n; i += gridDim.x)
+    chol_dd_unit(jobs, B, list[i], b_off, theta, ldth, out_units, scratch, scr_per_wg);
+}
+
+// The verify step: the forward (a) and reversed (b) fp64 factorisations of
+// units [u0, u0 + n) agree to a quarter of the strict bound of the unit's own
+// term (and on -inf), or the unit goes to the list for chol_dd_kernel.
+__global__ __launch_bounds__(256) void verify_units_kernel(const double* __restrict__ a, const double* __restrict__ b,
+                                                           long long u0, long long n, int* __restrict__ list,
+                                                           int* __restrict__ count) {
+  const long long i = (long long)blockIdx.x * 256 + threadIdx.x;
+  if (i >= n) return;
+  const long long u = u0 + i;
+  const double x = a[u], y = b[u];
+  const bool fx = x - x == 0.0, fy = y - y == 0.0;           // finite
+  const bool bad = (fx != fy) || (fx && fabs(x - y) > 0.25 * (1e-6 + 1e-10 * fabs(x)));
+  if (bad) list[atomicAdd(count, 1)] = (int)u;
 }
 
 }  // namespace
+
+int launch_verify_units(const double* a, const double* b, long long u0, long long n, int* list, int* count,
+                        hipStream_t st) {
+  if (n <= 0) return 0;
+  hipLaunchKernelGGL(verify_units_kernel, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, st, a, b, u0, n, list,
+                     count);
+  const hipError_t e = hipGetLastError();
+  return e == hipSuccess ? 0 : set_err(EWH_E_HIP, std::string("verify_units_kernel: ") + hipGetErrorString(e));
+}
 
 long long dd_scratch_per_wg(int ld) { return 2LL * ld * ld; }
 
@@ -115,7 +155,17 @@ int launch_chol_dd(const CholJob* jobs, int B, long long u0, long long n, int b_
                    double* units, double* scr, long long scr_per_wg, long long cap, hipStream_t st) {
   for (long long o = 0; o < n; o += cap)   // one scratch slot per workgroup of a launch
     hipLaunchKernelGGL(chol_dd_kernel, dim3((unsigned)std::min(cap, n - o)), dim3(256), 0, st, jobs, B, u0 + o, b_off,
-                       theta, ldth, units, scr, scr_per_wg);
+                       theta, ldth, units, scr, scr_per_wg, nullptr, nullptr);
+  const hipError_t e = hipGetLastError();
+  return e == hipSuccess ? 0 : set_err(EWH_E_HIP, std::string("chol_dd_kernel: ") + hipGetErrorString(e));
+}
+
+
+int launch_chol_dd_list(const CholJob* jobs, int B, int b_off, const double* theta, int ldth, double* units,
+                        double* scr, long long scr_per_wg, long long cap, const int* list, const int* count,
+                        hipStream_t st) {
+  hipLaunchKernelGGL(chol_dd_kernel, dim3((unsigned)cap), dim3(256), 0, st, jobs, B, 0LL, b_off, theta, ldth, units,
+                     scr, scr_per_wg, list, count);
   const hipError_t e = hipGetLastError();
   return e == hipSuccess ? 0 : set_err(EWH_E_HIP, std::string("chol_dd_kernel: ") + hipGetErrorString(e));
 }

@@ -35,7 +35,7 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(2, 2)))
 void chol_wide_kernel(const CholJob* __restrict__ jobs, int B, long long u0, int b_off,
                       const double* __restrict__ theta, int ldth, double* __restrict__ out_units,
                       double* __restrict__ scratch, long long scr_per_wg, int keep, double* __restrict__ keep_out,
-                      int keep_b0, int keep_bs) {
+                      int keep_b0, int keep_bs, int rev) {
   __shared__ double phinv[WIDE_LD_MAX];
   const int lane = threadIdx.x, q = lane >> 4, c = lane & 15;
   const long long u = u0 + xcd_unit(blockIdx.x, gridDim.x);
@@ -61,11 +61,15 @@ void chol_wide_kernel(const CholJob* __restrict__ jobs, int B, long long u0, int
   }
   const double lphi_sum = wave_sum(lphi.value());
   __syncthreads();
+  // rev (keep == 0 only): the same factorisation in the reversed column order
+  // (r stays last) -- pi(a) = LD - 2 - a -- an independent fp64 ordering of
+  // the same lnL, which the verify step compares with the forward one
+  auto pi = [&](int a) { return (rev && a < LD - 1) ? LD - 2 - a : a; };
 
   LogAcc ldet;
   bool ok = true;
   double qv = 0.0;
-  const int klast = __builtin_amdgcn_readfirstlane(J.mreal - 16 * (NB - 1));
+  const int klast = rev ? 16 : __builtin_amdgcn_readfirstlane(J.mreal - 16 * (NB - 1));
   const int KD = 16 * keep;
   double* ko = keep > 0 ? keep_out + ((long long)p * keep_bs + (b - keep_b0)) * ((long long)KD * KD) : nullptr;
 #pragma unroll 1
@@ -84,10 +88,10 @@ void chol_wide_kernel(const CholJob* __restrict__ jobs, int B, long long u0, int
         if (j < NB) {
           static_for<0, 4>([&](auto RR) {
             constexpr int r = decltype(RR)::value;
-            R[jj][r] = A[(long long)(16 * i + q + 4 * r) * LD + 16 * j + c];
+            R[jj][r] = A[(long long)pi(16 * i + q + 4 * r) * LD + pi(16 * j + c)];
           });
           if (j == i) {
-            const double pd = phinv[16 * i + c];
+            const double pd = phinv[pi(16 * i + c)];
             static_for<0, 4>([&](auto RR) {
               constexpr int r = decltype(RR)::value;
               R[jj][r] += (q + 4 * r == c) ? pd : 0.0;
@@ -167,10 +171,10 @@ long long wide_scratch_per_wg(int nb, int keep) {
 
 int launch_chol_wide(const CholJob* jobs, int B, long long u0, long long n, int b_off, const double* theta, int ldth,
                      double* units, double* scr, long long scr_per_wg, long long cap, int keep, double* keep_out,
-                     int keep_b0, int keep_bs, hipStream_t st) {
+                     int keep_b0, int keep_bs, hipStream_t st, int rev) {
   for (long long o = 0; o < n; o += cap)   // one scratch slot per workgroup of a launch
     hipLaunchKernelGGL(chol_wide_kernel, dim3((unsigned)std::min(cap, n - o)), dim3(64), 0, st, jobs, B, u0 + o, b_off,
-                       theta, ldth, units, scr, scr_per_wg, keep, keep_out, keep_b0, keep_bs);
+                       theta, ldth, units, scr, scr_per_wg, keep, keep_out, keep_b0, keep_bs, rev);
   const hipError_t e = hipGetLastError();
   return e == hipSuccess ? 0 : set_err(EWH_E_HIP, std::string("chol_wide_kernel: ") + hipGetErrorString(e));
 }

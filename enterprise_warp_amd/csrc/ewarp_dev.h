@@ -432,7 +432,7 @@ constexpr bool wave_uses(int nb, int wave, int j, int W = 4) {
 // per-tile weights); VW / WS: the virtual wave that picks the output blocks
 // (blocks VW + WS sl) and the virtual waves per sample -- WS = W SPLIT when a
 // sample's blocks are split over SPLIT workgroups (contract2_kernel).
-template <int NB, int WAVE, int W, int VW = WAVE, int WS = W>
+template <int NB, int WAVE, int W, int VW = WAVE, int WS = W, bool COMP = true>
 __device__ __forceinline__ void contract2_body(const PsrDev& P, const double* __restrict__ wrow,
                                                const double* __restrict__ brow, double* __restrict__ srow,
                                                double* __restrict__ Gout) {
@@ -467,6 +467,7 @@ __device__ __forceinline__ void contract2_body(const PsrDev& P, const double* __
     lo[sl] = v4d{0.0, 0.0, 0.0, 0.0};
   }
   auto flush = [&]() {
+    if constexpr (!COMP) return;
     static_for<0, SLOTS>([&](auto SL) {
       constexpr int sl = decltype(SL)::value;
       static_for<0, 4>([&](auto R) {
@@ -612,7 +613,7 @@ __device__ __forceinline__ void contract2_body(const PsrDev& P, const double* __
 #pragma unroll
     for (int r = 0; r < 4; ++r) {
       const int row = 16 * bi + q + 4 * r, col = 16 * bj + c;
-      double v = hi[decltype(SL)::value][r] + lo[decltype(SL)::value][r];
+      double v = COMP ? hi[decltype(SL)::value][r] + lo[decltype(SL)::value][r] : acc[decltype(SL)::value][r];
       if (row == col && row >= P.m && row < LD - 1) v = 1.0;
       Gout[(long long)row * LD + col] = v;
       Gout[(long long)col * LD + row] = v;
@@ -626,7 +627,7 @@ __device__ __forceinline__ void contract2_body(const PsrDev& P, const double* __
 // (blockIdx.y), each streaming the whole basis, so the three accumulator
 // sets of the compensated sum fit the register budget; each half has its own
 // epoch-sum scratch row (s_stride apart).
-template <int NB, int W, int SPLIT = 1>
+template <int NB, int W, int SPLIT = 1, bool COMP = true>
 __global__ __launch_bounds__(64 * W) void contract2_kernel(PsrDev P, const double* __restrict__ w,
                                                            const double* __restrict__ beta, double* __restrict__ s,
                                                            long long s_stride, double* __restrict__ G) {
@@ -640,13 +641,20 @@ __global__ __launch_bounds__(64 * W) void contract2_kernel(PsrDev P, const doubl
   static_for<0, SPLIT>([&](auto H) {
     static_for<0, W>([&](auto WV) {
       constexpr int h = decltype(H)::value, wave = decltype(WV)::value;
-      if (half == h && wv == wave) contract2_body<NB, wave, W, h * W + wave, W * SPLIT>(P, wrow, brow, srow, Gout);
+      if (half == h && wv == wave)
+        contract2_body<NB, wave, W, h * W + wave, W * SPLIT, COMP>(P, wrow, brow, srow, Gout);
     });
   });
 }
 // blocks of a sample split over two workgroups from this width on (the
 // compensated accumulators of 8 waves exceed 256 registers above NB = 10)
 constexpr int contract2_split(int nb) { return nb >= 11 ? 2 : 1; }
+// the compensated sum from this width on.  Below it (C2's 9 blocks) the
+// three accumulator sets would halve the occupancy (4 -> 2 waves per SIMD:
+// C2's contraction 18.2 -> 27.3 ms, profiles/r04*), and the single
+// accumulator already meets the per-sample accuracy bound there (c2_small,
+// the C2 bench draws); dev kernel mode 30 compensates every width
+constexpr bool contract2_comp(int nb) { return nb >= 10; }
 
 // ----------------------------------------------------------------------------
 // batched factorisation, MFMA register-blocked: one wave (64 lanes) per unit.
@@ -1416,9 +1424,18 @@ long long wide_scratch_per_wg(int nb, int keep);
 long long dd_scratch_per_wg(int ld);
 int launch_chol_dd(const CholJob* jobs, int B, long long u0, long long n, int b_off, const double* theta, int ldth,
                    double* units, double* scr, long long scr_per_wg, long long cap, hipStream_t st);
+// the verify-and-refine form: units a (forward fp64) vs b (reversed fp64) of
+// [u0, u0 + n) -> list / count of the disagreeing ones (count zeroed by the
+// caller), then chol_dd_kernel over the list (cap workgroups looping) into units
+int launch_verify_units(const double* a, const double* b, long long u0, long long n, int* list, int* count,
+                        hipStream_t st);
+int launch_chol_dd_list(const CholJob* jobs, int B, int b_off, const double* theta, int ldth, double* units,
+                        double* scr, long long scr_per_wg, long long cap, const int* list, const int* count,
+                        hipStream_t st);
+// rev = 1 (keep == 0): the reversed column order (the verify step)
 int launch_chol_wide(const CholJob* jobs, int B, long long u0, long long n, int b_off, const double* theta, int ldth,
                      double* units, double* scr, long long scr_per_wg, long long cap, int keep, double* keep_out,
-                     int keep_b0, int keep_bs, hipStream_t st);
+                     int keep_b0, int keep_bs, hipStream_t st, int rev = 0);
 // keep_out: pulsar-major kept blocks, keep_bs samples per pulsar (see chol_mfma_kernel KEEP)
 int launch_partial_nb(int nb, int keep, const CholJob* jobs, int B, long long u0, long long n, int b_off,
                       const double* theta, int ldth, double* units, double* keep_out, int keep_bs, hipStream_t st);

@@ -879,9 +879,11 @@ void dchol_rowupdate2_kernel(double* __restrict__ mats, int Np, int i) {
 // U_pk is staged through LDS (shared by the four waves), each wave's U_pj
 // slab comes from global memory into registers.  Same sums, same order as
 // dchol_rowupdate2_kernel + dchol_panel_reg_kernel: bit-identical.
-// TPW = 2 (dev A/B, kernel mode 28): two tiles (k, j), (k, j + 1) per
+// TPW = 2 (the default since round 4): two tiles (k, j), (k, j + 1) per
 // 8-wave workgroup sharing one LDS copy of U_pk -- per p the workgroup reads
-// 96 KB (U_pk + two U_pj) for two tiles instead of 64 KB for one.
+// 96 KB (U_pk + two U_pj) for two tiles instead of 64 KB for one; C5 at
+// B = 512: 91.3 vs 95.8 ms per batch, bit-identical (scripts/c5_ab.py).
+// TPW = 1: the round-3 form (dev kernel mode 28).
 template <int TPW>
 __global__ __launch_bounds__(256 * TPW) __attribute__((amdgpu_waves_per_eu(TPW == 1 ? 3 : 4, TPW == 1 ? 3 : 4)))
 void dchol_rowpanel_kernel(double* __restrict__ mats, int Np, int k, const double* __restrict__ wbuf) {
@@ -1173,6 +1175,10 @@ struct DevCtx {
   long long widescr_len = 0;     // doubles
   double* d_ddscr = nullptr;     // chol_dd_kernel: per-workgroup hi / lo matrices
   long long ddscr_len = 0;       // doubles
+  double* d_units2 = nullptr;    // the verify step's reversed-order unit terms
+  size_t units2_cap = 0;
+  int* d_ddlist = nullptr;       // the verify step's flagged units, [0] = count, list from [1]
+  size_t ddlist_cap = 0;
   double* d_Glo = nullptr;       // varying white noise, bases past 16 blocks: the low part of G (contract_wide_kernel)
   int chunk = 0;
   int chunk_cap = 0;          // largest chunk the ~1.5 GB scratch budget allows
@@ -1365,14 +1371,20 @@ void build_spec_rep(const std::vector<int>& ptr, const std::vector<DSpec>& ent, 
 
 // kernel mode 27: every factorisation (full and partial) by chol_wide_kernel
 // (routing only: the wide kernel is part of the product; tests compare it
-// with the register kernels)
-constexpr int MODE_WIDE = 27;
+// with the register kernels); 29: the double-double path for every unit it
+// covers, without the verify step
+constexpr int MODE_WIDE = 27, MODE_DD = 29;
 
 // The double-double factorisation (chol_dd_kernel) takes the uncorrelated
 // units the fp64 register kernels do not cover with fixed white noise
 // (reduced width > 9 blocks: the cached S is double-double) and every basis
 // wider than 16 blocks; kernel mode 27 routes them to the fp64 chol_wide
 // instead, mode 1 to the LDS kernel (A/B)
+// (MODE_DD: every unit in double-double; the default: verify-and-refine --
+// the forward and the reversed-order fp64 chol_wide factorisations, and
+// chol_dd_kernel only for the units on which they disagree by more than a
+// quarter of the strict bound: near-truth draws stay on fp64 MFMA, the
+// ill-conditioned prior draws get the double-double value)
 bool dd_path(const DevCtx* h, int nb, bool fixed) {
   if (h->corr || h->osmode || h->kernel_mode == MODE_WIDE || h->kernel_mode == 1) return false;
   return nb > BIG_NB_MAX || (fixed && nb > MFMA_NB_MAX);
@@ -1413,12 +1425,49 @@ long long ensure_wide_scratch(DevCtx* h, int nb, int keep) {
 }
 
 int launch_wide(DevCtx* h, int nb, int keep, const CholJob* jobs, int B, long long u0, long long n, int b_off,
-                const double* theta, int ldth, double* units, double* keep_out, hipStream_t st) {
+                const double* theta, int ldth, double* units, double* keep_out, hipStream_t st, int rev = 0) {
   if (nb > WIDE_NB_MAX) return set_err(EWH_E_UNSUPPORTED, "basis wider than 1023 columns");
   const long long cap = ensure_wide_scratch(h, nb, keep);
   if (cap <= 0) return EWH_E_NOMEM;
   return launch_chol_wide(jobs, B, u0, n, b_off, theta, ldth, units, h->d_widescr, wide_scratch_per_wg(nb, keep), cap,
-                          keep, keep_out, 0, B, st);
+                          keep, keep_out, 0, B, st, rev);
+}
+
+template <typename T>
+int ensure_buf(DevCtx* h, T** p, size_t* cap, size_t need) {
+  if (need <= *cap) return 0;
+  if (*p) {
+    (void)hipFree(*p);
+    h->allocs.erase(std::find(h->allocs.begin(), h->allocs.end(), (void*)*p));
+    *p = nullptr;
+  }
+  *cap = 0;
+  int rc = dalloc(h, p, need);
+  if (rc) return rc;
+  *cap = need;
+  return 0;
+}
+
+// The double-double path of units [u0, u0 + n) (dd_path): verify-and-refine
+// by default, every unit under MODE_DD
+int launch_dd_path(DevCtx* h, int nb, const CholJob* jobs, int B, long long u0, long long n, int b_off,
+                   const double* theta, int ldth, double* units, hipStream_t st) {
+  const long long cap = ensure_dd_scratch(h, 16 * nb);
+  if (cap <= 0) return EWH_E_NOMEM;
+  const long long per = dd_scratch_per_wg(16 * nb);
+  if (h->kernel_mode == MODE_DD)
+    return launch_chol_dd(jobs, B, u0, n, b_off, theta, ldth, units, h->d_ddscr, per, cap, st);
+  int rc;
+  const size_t U = (size_t)(h->P + (h->corr ? 1 : 0)) * B;
+  if ((rc = ensure_buf(h, &h->d_units2, &h->units2_cap, U)) || (rc = ensure_buf(h, &h->d_ddlist, &h->ddlist_cap, U + 1)))
+    return rc;
+  if ((rc = launch_wide(h, nb, 0, jobs, B, u0, n, b_off, theta, ldth, units, nullptr, st, 0)) ||
+      (rc = launch_wide(h, nb, 0, jobs, B, u0, n, b_off, theta, ldth, h->d_units2, nullptr, st, 1)))
+    return rc;
+  EWH_HIP(hipMemsetAsync(h->d_ddlist, 0, sizeof(int), st));
+  if ((rc = launch_verify_units(units, h->d_units2, u0, n, h->d_ddlist + 1, h->d_ddlist, st))) return rc;
+  return launch_chol_dd_list(jobs, B, b_off, theta, ldth, units, h->d_ddscr, per, std::min<long long>(cap, n),
+                             h->d_ddlist + 1, h->d_ddlist, st);
 }
 
 // the partial factorisation (correlated common process) of units [u0, u0 + n)
@@ -1436,11 +1485,7 @@ int dispatch_chol(DevCtx* h, int nb, int mreal, const CholJob* jobs, int B, long
                   const double* theta, int ldth, double* units, hipStream_t st, bool fixed) {
   if (n <= 0) return 0;
   const int mode = h->kernel_mode;
-  if (dd_path(h, nb, fixed)) {
-    const long long cap = ensure_dd_scratch(h, 16 * nb);
-    if (cap <= 0) return EWH_E_NOMEM;
-    return launch_chol_dd(jobs, B, u0, n, b_off, theta, ldth, units, h->d_ddscr, dd_scratch_per_wg(16 * nb), cap, st);
-  }
+  if (dd_path(h, nb, fixed)) return launch_dd_path(h, nb, jobs, B, u0, n, b_off, theta, ldth, units, st);
   if (mode == MODE_WIDE || nb > BIG_NB_MAX)
     return launch_wide(h, nb, 0, jobs, B, u0, n, b_off, theta, ldth, units, nullptr, st);
   double* bigscr = h->d_bigscr;
@@ -1550,7 +1595,8 @@ int run_white(DevCtx* h, int p, const double* theta, int ldth, int b0, int nb) {
                      h->d_beta, h->d_Kb, h->d_fac);
   if (ps.dev.n_bgroup == 0 && h->kernel_mode != 7 && ps.nb <= CONTRACT2_NB_MAX) {
     // (dev library A/B: mode 15 = 4 waves per sample, mode 16 = 8)
-    const int waves = h->kernel_mode == 15 ? 4 : h->kernel_mode == 16 ? 8 : 0;
+    // (30: the compensated sum at every width)
+    const int waves = h->kernel_mode == 15 ? 4 : h->kernel_mode == 16 ? 8 : h->kernel_mode == 30 ? 30 : 0;
     int rc = launch_contract2_nb(ps.nb, waves, ps.dev, h->d_w, h->d_beta, h->d_s, h->s_stride, h->d_G, nb, h->stream);
     if (rc) return rc;
     EWH_HIP(hipGetLastError());
@@ -1873,12 +1919,12 @@ int corr_finish(DevCtx* h, const double* theta_dev, int B, const double* keep, d
                              h->Np, k, h->d_wbuf, h->d_cldet, h->d_cq, h->d_cfail);
         if (m > 0 && fused)
         {
-          if (h->kernel_mode == 28)   // (dev A/B: two tiles per workgroup)
-            hipLaunchKernelGGL(HIP_KERNEL_NAME(dchol_rowpanel_kernel<2>), dim3((m + 1) / 2, nb), dim3(512), 0, st,
-                               h->d_dense, h->Np, k, h->d_wbuf);
-          else
+          if (h->kernel_mode == 28)   // (dev A/B: one tile per workgroup, the round-3 form)
             hipLaunchKernelGGL(HIP_KERNEL_NAME(dchol_rowpanel_kernel<1>), dim3(m, nb), dim3(256), 0, st, h->d_dense,
                                h->Np, k, h->d_wbuf);
+          else
+            hipLaunchKernelGGL(HIP_KERNEL_NAME(dchol_rowpanel_kernel<2>), dim3((m + 1) / 2, nb), dim3(512), 0, st,
+                               h->d_dense, h->Np, k, h->d_wbuf);
         }
         else if (m > 0)
           hipLaunchKernelGGL(dchol_panel_reg_kernel, dim3(4 * m, nb), dim3(64), 0, st, h->d_dense, h->Np, k,
@@ -2858,7 +2904,7 @@ int ewh_set_fixed_white(ewh_handle* H, const double* values) {
 
 int ewh_set_kernel_mode(ewh_handle* H, int32_t mode) {
   if (!H || mode < 0 || mode > 30) return set_err(EWH_E_INVALID, "bad handle / mode");
-  if (mode != 0 && mode != 1 && mode != 2 && mode != 7 && mode != MODE_WIDE && !variant_built(mode))
+  if (mode != 0 && mode != 1 && mode != 2 && mode != 7 && mode != MODE_WIDE && mode != MODE_DD && !variant_built(mode))
     return set_err(EWH_E_UNSUPPORTED, "kernel mode " + std::to_string(mode) +
                                           " is not built into this library (A/B variants: the dev library, make dev)");
   for (DevCtx* h : H->ctx) {

@@ -273,7 +273,10 @@ int ewh_transfer_stats(const ewh_handle* h, int64_t* h2d_bytes, int64_t* peer);
  * correlated common process also the round-1 dense LDS diagonal-block and
  * panel kernels), 27 = every factorisation (full and partial) by the fp64
  * any-width chol_wide_kernel (cross-check of the register, big and
- * double-double kernels), 7 = default factorisation with the round-1 kernels
+ * double-double kernels), 29 = the double-double factorisation for every unit
+ * of a basis past the register kernels (default: only where the forward and
+ * reversed fp64 factorisations disagree), 7 = default factorisation with the
+ * round-1 kernels
  * elsewhere: the contraction (varying white noise: separate epoch-sum
  * kernel, unpipelined tiles) instead of the pipelined one and, for a
  * correlated common process, the right-looking dense update and the LDS

@@ -112,7 +112,7 @@ def test_multi_context_theta_staging(require_gpu):
     columns once per context -- at most 1.2 x B x n_param x 8 bytes per
     batch, with the per-pulsar terms bit-identical to one context and peer
     access recorded for every context."""
-    c3s = synth.config_c3(n_psr=16, n_min=600, n_max=2400, epoch_size=8)
+    c3s = synth.config_c3(n_psr=45, n_min=300, n_max=1200, epoch_size=8)
     pta = c3s.pta
     B = 256
     X = synth.prior_draws(pta, B, 77)
@@ -125,7 +125,7 @@ def test_multi_context_theta_staging(require_gpu):
     print(f"theta bytes {nbytes} = {nbytes / full:.3f} x full, peer mask {peer:#x}")
     assert nbytes <= 1.2 * full
     assert peer == 0xff
-    check_parity(got, one, "C3-16psr on 8 contexts")
+    check_parity(got, one, "C3-45psr on 8 contexts")
     np.testing.assert_array_equal(eng.unit_terms(B), terms1)
     pta.engine(devices=[0])
 
@@ -298,6 +298,28 @@ def test_wide_kernel_matches_register_kernels(require_gpu, name):
     if name == "c4_small":
         tf = np.isfinite(ta)
         np.testing.assert_allclose(tb[tf], ta[tf], rtol=1e-14, atol=0)
+
+
+@pytest.mark.parametrize("name", ["c1_system", "c1_widefix", "c1_wide"])
+def test_dd_verify_and_refine(require_gpu, name):
+    """Bases past the register kernels (fixed white noise past 9 blocks,
+    any basis past 16): by default the forward and the reversed-order fp64
+    factorisations (chol_wide_kernel) verify each other and only the units
+    on which they disagree by more than a quarter of strict are refactored
+    in double-double (chol_dd_kernel); kernel mode 29 takes every unit
+    through chol_dd_kernel.  The two agree at the strict bound on every
+    golden sample (prior draws included)."""
+    from conftest import load_golden
+    pta, X, _, _ = load_golden(name)
+    eng = pta.engine()
+    eng.set_kernel_mode(2)
+    a = pta.get_lnlikelihood_batch(X)
+    eng.set_kernel_mode(29)
+    try:
+        b = pta.get_lnlikelihood_batch(X)
+    finally:
+        eng.set_kernel_mode(0)
+    check_parity(a, b, f"{name}: verify-and-refine vs double-double everywhere")
 
 
 def test_wide_bases_full_size(require_gpu):
