@@ -19,11 +19,12 @@ void launch_chol_mfma(const CholJob* jobs, int B, long long u0, long long n, int
 // (23: the latency kernel with every wait forced to run out, LAT_VAR_STALL;
 // 24, 25: latency-kernel variants, chol_lat.hip LAT_VAR_BARRIER / LAT_VAR_R3;
 // 26: one wave per SIMD, whole triangle resident, plain right-looking order;
-// 28: the C5 row update + panel with one tile per workgroup (round 3);
-// 30: the compensated contraction at every width)
+// 28: the C5 row update + panel with one tile per workgroup, one block row
+// per pass (round 3); 30: the compensated contraction at every width;
+// 31: the C5 row update one block row per pass, two tiles per workgroup)
 bool variant_built(int mode) {
   return mode == 15 || mode == 16 || mode == 17 || mode == 19 || mode == 21 || mode == 22 || mode == 23 ||
-         mode == 24 || mode == 25 || mode == 26 || mode == 28 || mode == 30;
+         mode == 24 || mode == 25 || mode == 26 || mode == 28 || mode == 30 || mode == 31;
 }
 // phase stamps of kernel mode 21 (g_stamps: STAMP_UNITS x STAMP_N)
 extern "C" int ewh_dev_stamps(long long* out, long long n) {

@@ -822,9 +822,10 @@ __global__ __launch_bounds__(256) void dchol_rowupdate_kernel(double* __restrict
 // of U_pi it multiplies, 16 doubles per lane -- straight from global memory
 // into registers, prefetched one step ahead together with the U_pj tile; the
 // minus sign is the MFMA neg modifier.  Same sums in the same order as
-// dchol_rowupdate_kernel: bit-identical.
+// dchol_rowupdate_kernel: bit-identical.  p0 > 0: only the rows p0 <= p < i
+// (the rest already applied by dchol_rowpair_kernel).
 __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(4, 4)))
-void dchol_rowupdate2_kernel(double* __restrict__ mats, int Np, int i) {
+void dchol_rowupdate2_kernel(double* __restrict__ mats, int Np, int i, int p0) {
   __shared__ double Uj[DCB][DCB + 1];
   const int j = i + blockIdx.x, bl = blockIdx.y, t = threadIdx.x;
   double* base = mats + (long long)bl * Np * Np;
@@ -846,8 +847,8 @@ void dchol_rowupdate2_kernel(double* __restrict__ mats, int Np, int i) {
 #pragma unroll
     for (int r = 0; r < 16; ++r) pb[r] = rp[(long long)(4 * r) * Np];
   };
-  if (i > 0) bload(0);
-  for (int p = 0; p < i; ++p) {
+  if (p0 < i) bload(p0);
+  for (int p = p0; p < i; ++p) {
     double a[16];
     const double* ap = acol + (long long)(DCB * p) * Np;
 #pragma unroll
@@ -883,10 +884,12 @@ void dchol_rowupdate2_kernel(double* __restrict__ mats, int Np, int i) {
 // 8-wave workgroup sharing one LDS copy of U_pk -- per p the workgroup reads
 // 96 KB (U_pk + two U_pj) for two tiles instead of 64 KB for one; C5 at
 // B = 512: 91.3 vs 95.8 ms per batch, bit-identical (scripts/c5_ab.py).
-// TPW = 1: the round-3 form (dev kernel mode 28).
+// TPW = 1: the round-3 form (dev kernel mode 28).  p0 > 0: only the rows
+// p0 <= p < k (dchol_rowpair_kernel applied the others; p0 = k: the panel
+// alone).
 template <int TPW>
 __global__ __launch_bounds__(256 * TPW) __attribute__((amdgpu_waves_per_eu(TPW == 1 ? 3 : 4, TPW == 1 ? 3 : 4)))
-void dchol_rowpanel_kernel(double* __restrict__ mats, int Np, int k, const double* __restrict__ wbuf) {
+void dchol_rowpanel_kernel(double* __restrict__ mats, int Np, int k, int p0, const double* __restrict__ wbuf) {
   constexpr int NT = 256 * TPW, RW = 64 / (NT / 64);   // threads; U_pk rows staged per thread
   __shared__ double Uk[DCB][DCB + 1];
   const int t = threadIdx.x, wave = t >> 6, tile = wave >> 2, w = wave & 3;
@@ -908,8 +911,8 @@ void dchol_rowpanel_kernel(double* __restrict__ mats, int Np, int k, const doubl
 #pragma unroll
     for (int r = 0; r < RW; ++r) pa[r] = rp[(long long)((NT / 64) * r) * Np];
   };
-  if (k > 0) aload(0);
-  for (int p = 0; p < k; ++p) {
+  if (p0 < k) aload(p0);
+  for (int p = p0; p < k; ++p) {
     double b[16];
     const double* bp = bcol + (long long)(DCB * p) * Np;
 #pragma unroll
@@ -951,6 +954,79 @@ void dchol_rowpanel_kernel(double* __restrict__ mats, int Np, int k, const doubl
   for (int s0 = 0; s0 < 4; ++s0)
 #pragma unroll
     for (int r = 0; r < 4; ++r) Akj[(long long)(16 * s0 + q + 4 * r) * Np + 16 * w + c] = acc[s0][r];
+}
+
+// The row update of two block rows at once -- a 128-row block row for the
+// update, whose cost is streaming the finished rows U_pj from HBM: tiles
+// (k, j) and (k + 1, j) for j > k take the updates of every row p < k, the
+// U_pj tile streamed once for both (twice the MFMA work per HBM byte of
+// dchol_rowpanel_kernel), U_pk and U_p,k+1 (adjacent; shared by every
+// workgroup of the sample, from L2) staged through LDS.  8 waves per column
+// tile j: wave w updates strip w & 3 (16 columns, all 64 rows) of tile
+// (k + (w >> 2), j); the two waves of a strip read the same U_pj slab (the
+// second read from L1 / L2).  The accumulators go back to HBM; row k then
+// runs its panel (dchol_rowpanel_kernel with p0 = k) and row k + 1 its last
+// update p = k (p0 = k) -- per tile the same MFMAs on the same operands in
+// the same order as the one-row schedule, the accumulator stored and
+// reloaded exactly in between: bit-identical (dev kernel mode 31 runs the
+// one-row schedule).
+__global__ __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(4, 4)))
+void dchol_rowpair_kernel(double* __restrict__ mats, int Np, int k) {
+  __shared__ double Uk[2][DCB][DCB + 1];
+  const int t = threadIdx.x, wave = t >> 6, rt = wave >> 2, w = wave & 3;
+  const int j = k + 1 + blockIdx.x, bl = blockIdx.y;
+  const int lane = t & 63, q = lane >> 4, c = lane & 15;
+  // every access as the sample's (uniform) base + a 32-bit byte offset (a
+  // sample's matrix is < 4 GB); the offsets pass through an empty asm where
+  // the compiler would otherwise keep one register per load live across the
+  // loop (which spills)
+  char* cb = (char*)(mats + (long long)bl * Np * Np);
+  auto at = [&](unsigned off) -> double& { return *(double*)(cb + off); };
+  const unsigned rowb = 8u * (unsigned)Np;                       // bytes per row
+  // this lane's element (q, c) of strip w of tile (k + rt, j)
+  const unsigned toff = (unsigned)(DCB * (k + rt) + q) * rowb + 8u * (unsigned)(DCB * j + 16 * w + c);
+  v4d acc[4];
+#pragma unroll
+  for (int s0 = 0; s0 < 4; ++s0)
+#pragma unroll
+    for (int r = 0; r < 4; ++r) acc[s0][r] = at(toff + (unsigned)(16 * s0 + 4 * r) * rowb);
+  const unsigned boff = (unsigned)q * rowb + 8u * (unsigned)(DCB * j + 16 * w + c);
+  // staging: thread t holds column (t & 127) of the 128-column pair, rows
+  // (t >> 7) + 4 r
+  const int scol = t & 127, srow = t >> 7, stile = scol >> 6, scc = scol & 63;
+  const unsigned aoff = 8u * (unsigned)(DCB * k + scol) + (unsigned)srow * rowb;
+  double pa[16];
+  auto aload = [&](int p) {
+    unsigned o = aoff + (unsigned)(DCB * p) * rowb;
+    asm volatile("" : "+v"(o));
+#pragma unroll
+    for (int r = 0; r < 16; ++r) pa[r] = at(o + (unsigned)(4 * r) * rowb);
+  };
+  if (k > 0) aload(0);
+  for (int p = 0; p < k; ++p) {
+    double b[16];
+    unsigned o = boff + (unsigned)(DCB * p) * rowb;
+    asm volatile("" : "+v"(o));
+#pragma unroll
+    for (int ts = 0; ts < 16; ++ts) b[ts] = at(o + (unsigned)(4 * ts) * rowb);
+    __syncthreads();
+#pragma unroll
+    for (int r = 0; r < 16; ++r) Uk[stile][srow + 4 * r][scc] = pa[r];
+    __syncthreads();
+    if (p + 1 < k) aload(p + 1);
+#pragma unroll
+    for (int ts = 0; ts < DCB / 4; ++ts) {
+#pragma unroll
+      for (int s0 = 0; s0 < 4; ++s0)
+        acc[s0] = __builtin_amdgcn_mfma_f64_16x16x4f64(Uk[rt][4 * ts + q][16 * s0 + c], b[ts], acc[s0], 0, 0, 1);
+    }
+  }
+  unsigned toff2 = toff;
+  asm volatile("" : "+v"(toff2));
+#pragma unroll
+  for (int s0 = 0; s0 < 4; ++s0)
+#pragma unroll
+    for (int r = 0; r < 4; ++r) at(toff2 + (unsigned)(16 * s0 + 4 * r) * rowb) = acc[s0][r];
 }
 
 // ----------------------------------------------------------------------------
@@ -1557,17 +1633,23 @@ int ensure_var_scratch(DevCtx* h, int B) {
   // contraction's last epoch tile reads zero-initialised pad rows
   const size_t sstride = ((maxe + CT_ROWS - 1) / CT_ROWS + 1) * CT_ROWS * maxld;
   const bool wide = maxld > 16 * BIG_NB_MAX;        // G_lo for the double-double factorisation
-  const size_t per = ((wide ? 2 : 1) * maxld * maxld + 2 * sstride + maxn + maxe + maxfac + 1) * sizeof(double);
-  const size_t cap = std::min<size_t>(1024, std::max<size_t>(1, (size_t)1536 * 1024 * 1024 / per));
+  // epoch-sum rows per sample: two when contract2_kernel splits a sample's
+  // blocks over two workgroups (one row per half)
+  size_t nsrow = 1;
+  for (auto& ps : h->psr)
+    if (ps.dev.n_bgroup == 0 && ps.nb <= CONTRACT2_NB_MAX && contract2_split(ps.nb) > 1) nsrow = 2;
+  const size_t per = ((wide ? 2 : 1) * maxld * maxld + nsrow * sstride + maxn + maxe + maxfac + 1) * sizeof(double);
+  size_t cap = std::min<size_t>(1024, std::max<size_t>(1, (size_t)1536 * 1024 * 1024 / per));
+  // whole rounds of workgroups over the 256 CUs (a chunk of 853 samples of
+  // C2 ran 2 rounds of 512 workgroups, the second two-thirds empty)
+  if (cap > 256) cap -= cap % 256;
   h->chunk_cap = (int)cap;
   const size_t chunk = std::min<size_t>(cap, (size_t)std::max(B, 1));
   int rc;
   if ((rc = dalloc(h, &h->d_w, chunk * maxn))) return rc;
   if ((rc = dalloc(h, &h->d_beta, chunk * maxe))) return rc;
-  // (x2: contract2_kernel with its blocks split over two workgroups per
-  // sample keeps one epoch-sum row per half)
-  if ((rc = dalloc(h, &h->d_s, 2 * chunk * sstride))) return rc;
-  EWH_HIP(hipMemset(h->d_s, 0, 2 * chunk * sstride * sizeof(double)));
+  if ((rc = dalloc(h, &h->d_s, nsrow * chunk * sstride))) return rc;
+  EWH_HIP(hipMemset(h->d_s, 0, nsrow * chunk * sstride * sizeof(double)));
   h->s_stride = (long long)sstride;
   if ((rc = dalloc(h, &h->d_G, chunk * maxld * maxld))) return rc;
   if ((rc = dalloc(h, &h->d_Kb, chunk))) return rc;
@@ -1900,11 +1982,21 @@ int corr_finish(DevCtx* h, const double* theta_dev, int B, const double* keep, d
       // of every tile in one launch, which shortens the dependent chain per
       // block row
       const bool fused = h->kernel_mode != 1 && h->kernel_mode != 7 && nb >= 64;
+      // two block rows per update pass (dchol_rowpair_kernel) for the large
+      // chunks: at an even k with a row k + 1 following, the rows p < k of
+      // both rows' tiles j > k first; row k + 1 then takes only p = k
+      const bool pairs = fused && h->kernel_mode != 28 && h->kernel_mode != 31;
+      int p0 = 0;                                       // the first row p this block row still needs
+      if (pairs && (k & 1)) p0 = k - 1;
+      if (pairs && !(k & 1) && m > 0 && k > 0)
+        hipLaunchKernelGGL(dchol_rowpair_kernel, dim3(m, nb), dim3(512), 0, st, h->d_dense, h->Np, k);
       if (h->kernel_mode == 1 && k > 0)     // round-1 row update (both operands staged through LDS)
         hipLaunchKernelGGL(dchol_rowupdate_kernel, dim3(m + 1, nb), dim3(256), 0, st, h->d_dense, h->Np, k);
       else if (k > 0 && h->kernel_mode != 7)   // the diagonal tile's row update only (fused), or the whole row
         hipLaunchKernelGGL(dchol_rowupdate2_kernel, dim3(fused ? 1 : m + 1, nb), dim3(256), 0, st, h->d_dense, h->Np,
-                           k);
+                           k, p0);
+      // (a row k whose rows p < k the pair kernel applied: the panel alone)
+      const int p0_panel = (pairs && !(k & 1) && m > 0) ? k : p0;
       if (h->kernel_mode == 7 || h->kernel_mode == 1) {   // A/B: round-1 LDS diagonal block + LDS-staged panel
         hipLaunchKernelGGL(dchol_diag_kernel, dim3(nb), dim3(256), 0, st, h->d_dense, h->Np, k, h->d_wbuf,
                            h->d_cldet, h->d_cq, h->d_cfail);
@@ -1919,12 +2011,12 @@ int corr_finish(DevCtx* h, const double* theta_dev, int B, const double* keep, d
                              h->Np, k, h->d_wbuf, h->d_cldet, h->d_cq, h->d_cfail);
         if (m > 0 && fused)
         {
-          if (h->kernel_mode == 28)   // (dev A/B: one tile per workgroup, the round-3 form)
+          if (h->kernel_mode == 28)   // (dev A/B: one tile per workgroup, one row per pass: the round-3 form)
             hipLaunchKernelGGL(HIP_KERNEL_NAME(dchol_rowpanel_kernel<1>), dim3(m, nb), dim3(256), 0, st, h->d_dense,
-                               h->Np, k, h->d_wbuf);
+                               h->Np, k, 0, h->d_wbuf);
           else
             hipLaunchKernelGGL(HIP_KERNEL_NAME(dchol_rowpanel_kernel<2>), dim3((m + 1) / 2, nb), dim3(512), 0, st,
-                               h->d_dense, h->Np, k, h->d_wbuf);
+                               h->d_dense, h->Np, k, p0_panel, h->d_wbuf);
         }
         else if (m > 0)
           hipLaunchKernelGGL(dchol_panel_reg_kernel, dim3(4 * m, nb), dim3(64), 0, st, h->d_dense, h->Np, k,

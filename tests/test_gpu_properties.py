@@ -265,6 +265,23 @@ def test_correlated_right_looking_small_chunks(require_gpu):
         np.testing.assert_array_equal(got, left)
 
 
+@pytest.mark.parametrize("n_psr", [16, 20])
+def test_correlated_row_pairs_bit_identical(require_gpu, n_psr):
+    """Chunks of >= 64 samples update two block rows of Sigma_c per pass
+    (dchol_rowpair_kernel: rows k, k + 1 take every p < k together, row
+    k + 1 then p = k); chunks of <= 4 factor right-looking.  Per tile the
+    same K = 64 slabs in the same order: bit-identical lnL.  16 pulsars: 8
+    block rows (the last pair ends the matrix), 20 pulsars: 9 (a single last
+    row)."""
+    cfg = synth.config_c5(n_psr=n_psr, n_toa=1200, seed=7)
+    pta = cfg.pta
+    X = synth.prior_draws(pta, 64, 11)
+    big = pta.get_lnlikelihood_batch(X)
+    small = np.concatenate([pta.get_lnlikelihood_batch(X[i:i + 4]) for i in range(0, 16, 4)])
+    assert np.all(np.isfinite(big[:16]))
+    np.testing.assert_array_equal(small, big[:16])
+
+
 @pytest.mark.parametrize("name", ["c4_small", "c3_small", "c2_small", "c5_small", "c5_varwn", "c1_system"])
 def test_wide_kernel_matches_register_kernels(require_gpu, name):
     """chol_wide_kernel (fp64, any width: the partial factorisation of a wide
