@@ -2995,7 +2995,7 @@ int ewh_set_fixed_white(ewh_handle* H, const double* values) {
 }
 
 int ewh_set_kernel_mode(ewh_handle* H, int32_t mode) {
-  if (!H || mode < 0 || mode > 30) return set_err(EWH_E_INVALID, "bad handle / mode");
+  if (!H || mode < 0 || mode > 31) return set_err(EWH_E_INVALID, "bad handle / mode");
   if (mode != 0 && mode != 1 && mode != 2 && mode != 7 && mode != MODE_WIDE && mode != MODE_DD && !variant_built(mode))
     return set_err(EWH_E_UNSUPPORTED, "kernel mode " + std::to_string(mode) +
                                           " is not built into this library (A/B variants: the dev library, make dev)");
