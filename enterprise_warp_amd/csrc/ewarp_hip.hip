@@ -358,30 +358,33 @@ __global__ __launch_bounds__(256) void common_minv_kernel(const CommonPsr* __res
   if (threadIdx.x == 0) mlog[(long long)bl * nc + slot] = ok ? lsum : __builtin_nan("");
 }
 
-// The same inverse for P <= MINV_PMAX with M held in registers: wave w owns
-// rows i = w + 4 r (r < MINV_PMAX / 4), lane l columns j = l + 64 cc (cc < 2).
-// Per pivot k the owners of column k and row k publish them to LDS (double
-// buffered by pivot parity: one barrier per pivot) and every thread updates
-// its elements in place -- no integer division or LDS round trip per element
-// (the LDS version above costs ~30x more on C5's 100 x 100 blocks).
+// The same inverse for P <= MINV_PMAX with M held in registers: 8 waves, wave
+// w owns rows i = w + 8 r (r < MINV_PMAX / 8), lane l columns j = l + 64 cc
+// (cc < 2).  Per pivot k the owners of column k and row k publish them to LDS
+// (double buffered by pivot parity: one barrier per pivot) and every thread
+// updates its elements in place.  The pivot loop is unrolled over the row
+// register r (k = 8 r + w_k), so row k's register and column k's half are
+// compile-time indices (the round-3 form, 4 waves with a runtime register
+// select and 338 registers at one wave per SIMD, took 6.7 ms per C5 batch of
+// 512; the same arithmetic in the same order: bit-identical).
 constexpr int MINV_PMAX = 128;
 // sample chunks up to this size factor Sigma_c right-looking (corr_finish)
 constexpr int CORR_RIGHT_LOOKING_MAX = 4;
 
-__global__ __launch_bounds__(256) void common_minv_reg_kernel(const CommonPsr* __restrict__ cps, int P,
+__global__ __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(4, 4))) void common_minv_reg_kernel(const CommonPsr* __restrict__ cps, int P,
                                                               const double* __restrict__ orf,
                                                               const DSpec* __restrict__ cspec, int nc,
                                                               const int* __restrict__ uniq,
                                                               const double* __restrict__ theta, int ldth, int b0,
                                                               double* __restrict__ minv, double* __restrict__ mlog) {
-  constexpr int RW = MINV_PMAX / 4;     // rows per wave
+  constexpr int NW = 8, RW = MINV_PMAX / NW;     // waves; rows per wave
   __shared__ double own[MINV_PMAX];
   __shared__ double colk[2][MINV_PMAX], rowk[2][MINV_PMAX];
   const int tid = threadIdx.x, w = tid >> 6, lane = tid & 63;
   const int slot = blockIdx.x, g = uniq[slot], bl = blockIdx.y;
   const double* th = theta + (long long)(b0 + bl) * ldth;
   const double pc = spec_phi(cspec[g], th);
-  for (int a = tid; a < P; a += 256) {
+  for (int a = tid; a < P; a += 64 * NW) {
     const CommonPsr c = cps[a];
     double v = 0.0;
     for (int e = c.colptr[c.gstart + g]; e < c.colptr[c.gstart + g + 1]; ++e) v += spec_phi(c.spec[e], th);
@@ -391,7 +394,7 @@ __global__ __launch_bounds__(256) void common_minv_reg_kernel(const CommonPsr* _
   double m[RW][2];
 #pragma unroll
   for (int r = 0; r < RW; ++r) {
-    const int i = w + 4 * r;
+    const int i = w + NW * r;
 #pragma unroll
     for (int cc = 0; cc < 2; ++cc) {
       const int j = lane + 64 * cc;
@@ -400,64 +403,50 @@ __global__ __launch_bounds__(256) void common_minv_reg_kernel(const CommonPsr* _
   }
   LogAcc lacc;
   bool ok = true;
-  for (int k = 0; k < P; ++k) {
-    const int buf = k & 1;
-    if (lane == (k & 63)) {               // column k: this lane, slot k / 64
-      const bool hi = k >= 64;
+  static_for<0, RW>([&](auto R) {
+    constexpr int r = decltype(R)::value;
+    constexpr int cc = (NW * r) >= 64 ? 1 : 0;     // column k = NW r + wk lies in half cc
+#pragma unroll 1
+    for (int wk = 0; wk < NW; ++wk) {
+      const int k = NW * r + wk;
+      if (k >= P) break;
+      const int buf = k & 1;
+      const bool colown = lane == (k & 63);
+      if (colown) {                                  // column k: one lane per wave
 #pragma unroll
-      for (int r = 0; r < RW; ++r) colk[buf][w + 4 * r] = hi ? m[r][1] : m[r][0];
-    }
-    if (w == (k & 3)) {                   // row k: this wave, register k / 4
-      const int rk = k >> 2;
+        for (int r2 = 0; r2 < RW; ++r2) colk[buf][w + NW * r2] = m[r2][cc];
+      }
+      if (w == wk) {                                 // row k: this wave, register r
+        rowk[buf][lane] = m[r][0];
+        rowk[buf][lane + 64] = m[r][1];
+      }
+      __syncthreads();
+      const double piv = rowk[buf][k];
+      ok = ok && (piv > 0.0);
+      lacc.add(piv);
+      const double pinv = 1.0 / piv;
+      const double rj0 = rowk[buf][lane] * pinv, rj1 = rowk[buf][lane + 64] * pinv;
+      double ci[RW];                                 // (all reads first: one LDS wait)
 #pragma unroll
-      for (int r = 0; r < RW; ++r)
-        if (r == rk) {
-          rowk[buf][lane] = m[r][0];
-          rowk[buf][lane + 64] = m[r][1];
-        }
-    }
-    __syncthreads();
-    const double piv = rowk[buf][k];
-    ok = ok && (piv > 0.0);
-    lacc.add(piv);
-    const double pinv = 1.0 / piv;
-    const double rj0 = rowk[buf][lane] * pinv, rj1 = rowk[buf][lane + 64] * pinv;
-    double ci[RW];
+      for (int r2 = 0; r2 < RW; ++r2) ci[r2] = colk[buf][w + NW * r2];
 #pragma unroll
-    for (int r = 0; r < RW; ++r) {
-      ci[r] = colk[buf][w + 4 * r];
-      m[r][0] = fma(-ci[r], rj0, m[r][0]);
-      m[r][1] = fma(-ci[r], rj1, m[r][1]);
-    }
-    // column k (one lane per wave): -M[i][k] / piv; then row k: M[k][j] / piv
-    // and the pivot 1 / piv (uniform branches on k, one divergent lane test)
-    if (lane == (k & 63)) {
-      if (k < 64) {
-#pragma unroll
-        for (int r = 0; r < RW; ++r) m[r][0] = -ci[r] * pinv;
-      } else {
-#pragma unroll
-        for (int r = 0; r < RW; ++r) m[r][1] = -ci[r] * pinv;
+      for (int r2 = 0; r2 < RW; ++r2) {
+        const double u0 = fma(-ci[r2], rj0, m[r2][0]), u1 = fma(-ci[r2], rj1, m[r2][1]);
+        const double cv = -ci[r2] * pinv;            // column k: -M[i][k] / piv (a select, no branch)
+        m[r2][0] = (cc == 0 && colown) ? cv : u0;
+        m[r2][1] = (cc == 1 && colown) ? cv : u1;
+      }
+      if (w == wk) {                                 // row k: M[k][j] / piv, the pivot 1 / piv
+        m[r][0] = rj0;
+        m[r][1] = rj1;
+        if (colown) m[r][cc] = pinv;
       }
     }
-    if (w == (k & 3)) {
-      const int rk = k >> 2;
-#pragma unroll
-      for (int r = 0; r < RW; ++r)
-        if (r == rk) {
-          m[r][0] = rj0;
-          m[r][1] = rj1;
-          if (lane == (k & 63)) {
-            if (k < 64) m[r][0] = pinv;
-            else m[r][1] = pinv;
-          }
-        }
-    }
-  }
+  });
   double* out = minv + ((long long)bl * nc + slot) * P * P;
 #pragma unroll
   for (int r = 0; r < RW; ++r) {
-    const int i = w + 4 * r;
+    const int i = w + NW * r;
 #pragma unroll
     for (int cc = 0; cc < 2; ++cc) {
       const int j = lane + 64 * cc;
@@ -467,17 +456,24 @@ __global__ __launch_bounds__(256) void common_minv_reg_kernel(const CommonPsr* _
   if (tid == 0) mlog[(long long)bl * nc + slot] = ok ? lacc.value() : __builtin_nan("");
 }
 
-// Dense Sigma_c (Np x Np, row-major) of sample bl, one row per workgroup:
-// rows/cols (a, g) -> a nc + g; r at Np - 1; pad rows/cols identity.
-// keep: pulsar-major kept blocks, Bk samples per pulsar; this chunk starts at
-// sample b0 (pulsar a's block of sample bl at keep[(a Bk + b0 + bl) KD^2]).
+// Dense Sigma_c (Np x Np, row-major) of sample bl, one row per wave (four
+// per workgroup): rows/cols (a, g) -> a nc + g; r at Np - 1; pad rows/cols
+// identity.  keep: pulsar-major kept blocks, Bk samples per pulsar; this chunk
+// starts at sample b0 (pulsar a's block of sample bl at keep[(a Bk + b0 + bl)
+// KD^2]).  Column j -> (pulsar, common column) by a float reciprocal (exact:
+// (j + 1/2) / nc is at least 1/(2 nc) from an integer) instead of an integer
+// division per element.
+__device__ __forceinline__ int div_nc(int j, float rnc) { return (int)(((float)j + 0.5f) * rnc); }
+
 __global__ __launch_bounds__(256) void common_assemble_kernel(const double* __restrict__ keep, int KD, int P, int nc,
                                                               long long Bk, int b0,
                                                               const double* __restrict__ minv,
                                                               const int* __restrict__ rep, int Np,
                                                               double* __restrict__ mats) {
-  const int i = blockIdx.x, bl = blockIdx.y;
+  const int i = 4 * blockIdx.x + (threadIdx.x >> 6), lane = threadIdx.x & 63, bl = blockIdx.y;
+  if (i >= Np) return;
   const int N = P * nc;
+  const float rnc = 1.0f / (float)nc;
   const long long ps = Bk * KD * KD;                                // pulsar stride
   double* row = mats + ((long long)bl * Np + i) * Np;
   const double* kb = keep + (long long)(b0 + bl) * KD * KD;
@@ -486,13 +482,13 @@ __global__ __launch_bounds__(256) void common_assemble_kernel(const double* __re
   // are ever read by the factorisation: the rest of the row is not written
   const int j0 = (i / DCB) * DCB;
   if (i < N) {
-    const int a = i / nc, g = i - a * nc;
+    const int a = div_nc(i, rnc), g = i - a * nc;
     const double* ka = kb + (long long)a * ps + g * KD;            // row g of pulsar a's kept square
     const double* mg = mb + (long long)rep[g] * P * P + (long long)a * P;  // row a of M_g^-1
-    for (int j = j0 + threadIdx.x; j < Np; j += 256) {
+    for (int j = j0 + lane; j < Np; j += 64) {
       double v = 0.0;
       if (j < N) {
-        const int bb = j / nc, h = j - bb * nc;
+        const int bb = div_nc(j, rnc), h = j - bb * nc;
         if (bb == a) v = ka[h];
         if (h == g) v += mg[bb];
       } else if (j == Np - 1) {
@@ -501,10 +497,10 @@ __global__ __launch_bounds__(256) void common_assemble_kernel(const double* __re
       row[j] = v;
     }
   } else if (i == Np - 1) {
-    for (int j = j0 + threadIdx.x; j < Np; j += 256) {
+    for (int j = j0 + lane; j < Np; j += 64) {
       double v = 0.0;
       if (j < N) {
-        const int bb = j / nc, h = j - bb * nc;
+        const int bb = div_nc(j, rnc), h = j - bb * nc;
         v = kb[(long long)bb * ps + (KD - 1) * KD + h];
       } else if (j == Np - 1) {
         for (int a = 0; a < P; ++a) v += kb[(long long)a * ps + KD * KD - 1];
@@ -512,7 +508,7 @@ __global__ __launch_bounds__(256) void common_assemble_kernel(const double* __re
       row[j] = v;
     }
   } else {
-    for (int j = j0 + threadIdx.x; j < Np; j += 256) row[j] = (j == i) ? 1.0 : 0.0;
+    for (int j = j0 + lane; j < Np; j += 64) row[j] = (j == i) ? 1.0 : 0.0;
   }
 }
 
@@ -964,14 +960,15 @@ void dchol_rowpanel_kernel(double* __restrict__ mats, int Np, int k, int p0, con
 // workgroup of the sample, from L2) staged through LDS.  8 waves per column
 // tile j: wave w updates strip w & 3 (16 columns, all 64 rows) of tile
 // (k + (w >> 2), j); the two waves of a strip read the same U_pj slab (the
-// second read from L1 / L2).  The accumulators go back to HBM; row k then
-// runs its panel (dchol_rowpanel_kernel with p0 = k) and row k + 1 its last
-// update p = k (p0 = k) -- per tile the same MFMAs on the same operands in
-// the same order as the one-row schedule, the accumulator stored and
-// reloaded exactly in between: bit-identical (dev kernel mode 31 runs the
-// one-row schedule).
+// second read from L1 / L2).  Launched after dchol_diag_reg_kernel has
+// factored tile (k, k): the row-k waves finish with the panel (U_kj written
+// once, as dchol_rowpanel_kernel), the row-(k + 1) accumulators go back to
+// HBM and row k + 1 takes its last update p = k in dchol_rowpanel_kernel
+// (p0 = k) -- per tile the same MFMAs on the same operands in the same order
+// as the one-row schedule, the accumulator stored and reloaded exactly in
+// between: bit-identical (dev kernel mode 31 runs the one-row schedule).
 __global__ __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(4, 4)))
-void dchol_rowpair_kernel(double* __restrict__ mats, int Np, int k) {
+void dchol_rowpair_kernel(double* __restrict__ mats, int Np, int k, const double* __restrict__ wbuf) {
   __shared__ double Uk[2][DCB][DCB + 1];
   const int t = threadIdx.x, wave = t >> 6, rt = wave >> 2, w = wave & 3;
   const int j = k + 1 + blockIdx.x, bl = blockIdx.y;
@@ -1020,6 +1017,29 @@ void dchol_rowpair_kernel(double* __restrict__ mats, int Np, int k) {
       for (int s0 = 0; s0 < 4; ++s0)
         acc[s0] = __builtin_amdgcn_mfma_f64_16x16x4f64(Uk[rt][4 * ts + q][16 * s0 + c], b[ts], acc[s0], 0, 0, 1);
     }
+  }
+  if (rt == 0) {
+    // row k is complete: its panel U_kj = L_kk^-1 A_kj on this strip, with the
+    // operands dchol_diag_reg_kernel left in wbuf (as dchol_rowpanel_kernel)
+    const double* W = wbuf + (long long)bl * DW_SLOTS * 256 + lane * 4;
+    static_for<0, 4>([&](auto SS) {
+      constexpr int s0 = decltype(SS)::value;
+      static_for<0, s0>([&](auto TT) {
+        constexpr int t0 = decltype(TT)::value;
+        syrk_update(acc[s0], *(const v4d*)(W + dw_u(t0, s0) * 256), acc[t0]);
+      });
+      const v4d E = *(const v4d*)(W + s0 * 256);
+      const v4d rs = *(const v4d*)(W + (4 + s0) * 256);
+      v4d v = {0.0, 0.0, 0.0, 0.0};
+      static_for<0, 4>([&](auto S2) {
+        constexpr int sk = decltype(S2)::value;
+        v = __builtin_amdgcn_mfma_f64_16x16x4f64(E[sk], acc[s0][sk], v, 0, 0, 0);
+      });
+      static_for<0, 4>([&](auto R) {
+        constexpr int r = decltype(R)::value;
+        acc[s0][r] = v[r] * rs[r];
+      });
+    });
   }
   unsigned toff2 = toff;
   asm volatile("" : "+v"(toff2));
@@ -1946,12 +1966,12 @@ int corr_finish(DevCtx* h, const double* theta_dev, int B, const double* keep, d
   for (int c0 = 0; c0 < B; c0 += h->cchunk) {
     const int nb = std::min(h->cchunk, B - c0);
     if (P <= MINV_PMAX && h->kernel_mode != 7)
-      hipLaunchKernelGGL(common_minv_reg_kernel, dim3(h->nuniq, nb), dim3(256), 0, st, h->d_cps, P, h->d_orf,
+      hipLaunchKernelGGL(common_minv_reg_kernel, dim3(h->nuniq, nb), dim3(512), 0, st, h->d_cps, P, h->d_orf,
                          h->d_cspec, h->nc, h->d_cuniq, theta_dev, ldth, c0, h->d_minv, h->d_mlog);
     else
       hipLaunchKernelGGL(common_minv_kernel, dim3(h->nuniq, nb), dim3(256), lds, st, h->d_cps, P, h->d_orf,
                          h->d_cspec, h->nc, h->d_cuniq, theta_dev, ldth, c0, h->d_minv, h->d_mlog);
-    hipLaunchKernelGGL(common_assemble_kernel, dim3(h->Np, nb), dim3(256), 0, st, keep, KD, P, h->nc,
+    hipLaunchKernelGGL(common_assemble_kernel, dim3((h->Np + 3) / 4, nb), dim3(256), 0, st, keep, KD, P, h->nc,
                        (long long)B, c0, h->d_minv, h->d_crep, h->Np, h->d_dense);
     EWH_HIP(hipMemsetAsync(h->d_cldet, 0, sizeof(double) * nb, st));
     EWH_HIP(hipMemsetAsync(h->d_cq, 0, sizeof(double) * nb, st));
@@ -1988,15 +2008,13 @@ int corr_finish(DevCtx* h, const double* theta_dev, int B, const double* keep, d
       const bool pairs = fused && h->kernel_mode != 28 && h->kernel_mode != 31;
       int p0 = 0;                                       // the first row p this block row still needs
       if (pairs && (k & 1)) p0 = k - 1;
-      if (pairs && !(k & 1) && m > 0 && k > 0)
-        hipLaunchKernelGGL(dchol_rowpair_kernel, dim3(m, nb), dim3(512), 0, st, h->d_dense, h->Np, k);
+      const bool pair_here = pairs && !(k & 1) && m > 0 && k > 0;
       if (h->kernel_mode == 1 && k > 0)     // round-1 row update (both operands staged through LDS)
         hipLaunchKernelGGL(dchol_rowupdate_kernel, dim3(m + 1, nb), dim3(256), 0, st, h->d_dense, h->Np, k);
       else if (k > 0 && h->kernel_mode != 7)   // the diagonal tile's row update only (fused), or the whole row
         hipLaunchKernelGGL(dchol_rowupdate2_kernel, dim3(fused ? 1 : m + 1, nb), dim3(256), 0, st, h->d_dense, h->Np,
                            k, p0);
-      // (a row k whose rows p < k the pair kernel applied: the panel alone)
-      const int p0_panel = (pairs && !(k & 1) && m > 0) ? k : p0;
+
       if (h->kernel_mode == 7 || h->kernel_mode == 1) {   // A/B: round-1 LDS diagonal block + LDS-staged panel
         hipLaunchKernelGGL(dchol_diag_kernel, dim3(nb), dim3(256), 0, st, h->d_dense, h->Np, k, h->d_wbuf,
                            h->d_cldet, h->d_cq, h->d_cfail);
@@ -2014,9 +2032,11 @@ int corr_finish(DevCtx* h, const double* theta_dev, int B, const double* keep, d
           if (h->kernel_mode == 28)   // (dev A/B: one tile per workgroup, one row per pass: the round-3 form)
             hipLaunchKernelGGL(HIP_KERNEL_NAME(dchol_rowpanel_kernel<1>), dim3(m, nb), dim3(256), 0, st, h->d_dense,
                                h->Np, k, 0, h->d_wbuf);
+          else if (pair_here)         // rows k and k + 1 over p < k, row k's panel
+            hipLaunchKernelGGL(dchol_rowpair_kernel, dim3(m, nb), dim3(512), 0, st, h->d_dense, h->Np, k, h->d_wbuf);
           else
             hipLaunchKernelGGL(HIP_KERNEL_NAME(dchol_rowpanel_kernel<2>), dim3((m + 1) / 2, nb), dim3(512), 0, st,
-                               h->d_dense, h->Np, k, p0_panel, h->d_wbuf);
+                               h->d_dense, h->Np, k, p0, h->d_wbuf);
         }
         else if (m > 0)
           hipLaunchKernelGGL(dchol_panel_reg_kernel, dim3(4 * m, nb), dim3(64), 0, st, h->d_dense, h->Np, k,
