@@ -494,7 +494,7 @@ __global__ __launch_bounds__(256) void common_assemble_kernel(const double* __re
       } else if (j == Np - 1) {
         v = ka[KD - 1];
       }
-      row[j] = v;
+      __builtin_nontemporal_store(v, row + j);
     }
   } else if (i == Np - 1) {
     for (int j = j0 + lane; j < Np; j += 64) {
@@ -505,10 +505,10 @@ __global__ __launch_bounds__(256) void common_assemble_kernel(const double* __re
       } else if (j == Np - 1) {
         for (int a = 0; a < P; ++a) v += kb[(long long)a * ps + KD * KD - 1];
       }
-      row[j] = v;
+      __builtin_nontemporal_store(v, row + j);
     }
   } else {
-    for (int j = j0 + lane; j < Np; j += 64) row[j] = (j == i) ? 1.0 : 0.0;
+    for (int j = j0 + lane; j < Np; j += 64) __builtin_nontemporal_store((j == i) ? 1.0 : 0.0, row + j);
   }
 }
 
