@@ -817,6 +817,19 @@ __device__ __forceinline__ void repl_rows_update(double (&Rr)[4], double nw) {
 // latency in front of the reciprocal: 3.70 vs 3.65 ms per launch; masking
 // only the high dword of the E multiplier -- one v_cndmask_b32 less -- 3.70
 // ms.  Neither is kept.)
+// __shfl(x, 16 KQ + c) with the lane address formed at the use: an empty asm
+// keeps the compiler from carrying the address of one KQ across the whole
+// kernel (in the headline kernel's last block row it did, and spilled it:
+// VERDICT r03 item 2)
+template <int KQ>
+__device__ __forceinline__ double shfl_row_fresh(double x, int c) {
+  int a = c << 2;
+  asm volatile("" : "+v"(a));
+  const int lo = __builtin_amdgcn_ds_bpermute(a + 64 * KQ, __double2loint(x));
+  const int hi = __builtin_amdgcn_ds_bpermute(a + 64 * KQ, __double2hiint(x));
+  return __hiloint2double(hi, lo);
+}
+
 template <int NB, int BB, bool RL, bool REPL = false>
 __device__ __forceinline__ void diag_factor_2l(v4d& D, v4d& E, double (&rsr)[4], int q, int c, LogAcc& ldet,
                                                bool& ok, int klim) {
@@ -844,7 +857,7 @@ __device__ __forceinline__ void diag_factor_2l(v4d& D, v4d& E, double (&rsr)[4],
         if (k >= klim) return;                         // wave-uniform: pad pivots
       }
       constexpr bool doe = !LASTR && k < 15;
-      const double xk = REPL ? Rr[kq] : __shfl(D[kr], 16 * kq + c);    // A[k][c]
+      const double xk = REPL ? Rr[kq] : LASTR ? shfl_row_fresh<kq>(D[kr], c) : __shfl(D[kr], 16 * kq + c);  // A[k][c]
       const double d = REPL ? readlane_d(Rr[kq], k) : readlane_d(D[kr], 16 * kq + k);
       const double nw = div_fast(-xk, d);
       const double nwm = (doe && c > k) ? nw : 0.0;
@@ -1228,13 +1241,15 @@ void chol_mfma_kernel(const CholJob* __restrict__ jobs, int B, long long u0, int
   } else {
     constexpr int KD = 16 * KEEP;
     double* ko = keep_out + ((long long)p * keep_bs + (b - keep_b0)) * (KD * KD);
+    int qo = q, co = c;                     // (store addresses formed here, not hoisted: they spilled)
+    asm volatile("" : "+v"(qo), "+v"(co));
     static_for<NB - KEEP, NB>([&](auto II) {
       constexpr int i = decltype(II)::value;
       static_for<i, NB>([&](auto JJ) {
         constexpr int j = decltype(JJ)::value;
         static_for<0, 4>([&](auto RR) {
           constexpr int r = decltype(RR)::value;
-          const int row = 16 * (i - (NB - KEEP)) + q + 4 * r, col = 16 * (j - (NB - KEEP)) + c;
+          const int row = 16 * (i - (NB - KEEP)) + qo + 4 * r, col = 16 * (j - (NB - KEEP)) + co;
           const double v = U2[S::i2(i, j)][r];
           if (i != j || row <= col) {
             ko[row * KD + col] = v;

@@ -444,13 +444,15 @@ __global__ __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(4, 4))) voi
     }
   });
   double* out = minv + ((long long)bl * nc + slot) * P * P;
+  int o0 = w * P + lane;              // (formed here: addresses carried from the loads spill)
+  asm volatile("" : "+v"(o0));
 #pragma unroll
   for (int r = 0; r < RW; ++r) {
     const int i = w + NW * r;
 #pragma unroll
     for (int cc = 0; cc < 2; ++cc) {
       const int j = lane + 64 * cc;
-      if (i < P && j < P) out[i * P + j] = m[r][cc];
+      if (i < P && j < P) out[o0 + NW * r * P + 64 * cc] = m[r][cc];
     }
   }
   if (tid == 0) mlog[(long long)bl * nc + slot] = ok ? lacc.value() : __builtin_nan("");
