@@ -29,6 +29,7 @@ pmc() {  # pmc <name> <script args> -- counters...
 run make 600 make -C enterprise_warp_amd/csrc -j16 all dev
 test -f enterprise_warp_amd/libewarp_hip_dev.so || { echo "dev library missing: stopping"; exit 1; }
 python -c "import bench; print('kernel sources sha', bench.kernel_sources_sha())" > gpurun_out/kernel_sources_sha_$TAG.txt
+cp gpurun_out/kernel_sources_sha_$TAG.txt gpurun_out/pmc_${TAG}_sha.txt   # (read by scripts/pmc_summary.py)
 run bench 400 python bench.py --steps 20 --warmup 3 --cpu-seconds 10
 run rocprof 300 rocprofv3 --kernel-trace --stats -d gpurun_out/prof_$TAG -o run --output-format csv -- python bench.py --steps 20 --warmup 3 --no-cpu-baseline --no-latency
 run configs 400 rocprofv3 --kernel-trace --stats -d gpurun_out/profcfg_$TAG -o run --output-format csv -- python scripts/bench_configs.py --configs c2,c3,c4 --reps 3 --check 3
@@ -41,4 +42,10 @@ CF="scripts/bench_configs.py --configs c2,c4 --reps 1 --check 1"
 pmc csq "$CF" SQ_VALU_MFMA_BUSY_CYCLES SQ_INSTS_MFMA SQ_INSTS_VALU SQ_INSTS_LDS SQ_WAVE_CYCLES SQ_BUSY_CYCLES GRBM_GUI_ACTIVE
 pmc cfetch "$CF" FETCH_SIZE
 pmc cwrite "$CF" WRITE_SIZE
+# C5 (HD, 100 psr x 20k TOAs, B = 512): kernel stats and the pair kernel's counters
+run c5prof 300 rocprofv3 --kernel-trace --stats -d gpurun_out/profc5_$TAG -o run --output-format csv -- python scripts/c5_ab.py --modes 0 --rounds 2
+C5="scripts/c5_ab.py --modes 0 --rounds 1"
+pmc c5sq "$C5" SQ_VALU_MFMA_BUSY_CYCLES SQ_INSTS_MFMA SQ_INSTS_VALU SQ_INSTS_LDS SQ_WAVE_CYCLES SQ_BUSY_CYCLES GRBM_GUI_ACTIVE
+pmc c5fetch "$C5" FETCH_SIZE
+pmc c5write "$C5" WRITE_SIZE
 echo PROFILE_DONE

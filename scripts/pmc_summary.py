@@ -31,7 +31,7 @@ def short(name):
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("tag")
-    ap.add_argument("--kernel", default="chol_mfma_kernel")
+    ap.add_argument("--kernel", default="chol_mfma_kernel<8, 2, 25, false, 0,")   # (the headline; not the C5 KEEP form)
     ap.add_argument("--src", default=os.path.join(ROOT, "gpurun_out"))
     args = ap.parse_args()
     per = collections.defaultdict(lambda: collections.defaultdict(list))
