@@ -35,7 +35,9 @@ def main():
     for src, name in ((f"prof_{tag}/run_kernel_stats.csv", "kernel_stats_bench.csv"),
                       (f"prof_{tag}/run_domain_stats.csv", "domain_stats_bench.csv"),
                       (f"profcfg_{tag}/run_kernel_stats.csv", "kernel_stats_configs.csv"),
-                      (f"bench_{tag}.log", "bench.log"), (f"configs_{tag}.log", "configs.log")):
+                      (f"bench_{tag}.log", "bench.log"), (f"configs_{tag}.log", "configs.log"),
+                      (f"profc5_{tag}/run_kernel_stats.csv", "kernel_stats_c5_b512.csv"),
+                      (f"c5prof_{tag}.log", "c5_ab.log"), (f"kernel_sources_sha_{tag}.txt", "kernel_sources_sha.txt")):
         p = os.path.join(OUT, src)
         if os.path.exists(p):
             shutil.copy(p, os.path.join(dst, name))
