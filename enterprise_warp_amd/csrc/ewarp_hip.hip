@@ -855,11 +855,7 @@ void dchol_rowupdate2_kernel(double* __restrict__ mats, int Np, int i, int p0) {
 #pragma unroll
     for (int r = 0; r < 16; ++r) Uj[(t >> 6) + 4 * r][t & 63] = pb[r];
     __syncthreads();
-    // (unconditional -- the last step reloads its own rows: with a branch the
-    // waitcnt pass merges the two paths and makes the MFMAs below wait for the
-    // first prefetched load too, exposing its latency every step)
-    bload(min(p + 1, i - 1));
-    asm volatile("" ::: "memory");
+    if (p + 1 < i) bload(p + 1);
 #pragma unroll
     for (int ts = 0; ts < DCB / 4; ++ts) {
 #pragma unroll
@@ -923,13 +919,10 @@ void dchol_rowpanel_kernel(double* __restrict__ mats, int Np, int k, int p0, con
 #pragma unroll
     for (int r = 0; r < RW; ++r) Uk[(t >> 6) + (NT / 64) * r][t & 63] = pa[r];
     __syncthreads();
-    // (unconditional -- the last step reloads its own rows: with a branch the
-    // waitcnt pass merges the two paths and makes the MFMAs below wait for the
-    // first prefetched load too; the empty asm keeps the compiler from sinking
-    // the prefetch to its use in the next step, where its latency would be
-    // exposed again)
-    aload(min(p + 1, k - 1));
-    asm volatile("" ::: "memory");
+    // (measured round 4: forcing a true one-step-ahead prefetch here -- an
+    // unconditional load pinned by an empty asm -- ran C5 at 89.9 instead of
+    // 83.6 ms; as written the compiler issues it with the next step's loads)
+    if (p + 1 < k) aload(p + 1);
 #pragma unroll
     for (int ts = 0; ts < DCB / 4; ++ts) {
 #pragma unroll
@@ -1022,13 +1015,10 @@ void dchol_rowpair_kernel(double* __restrict__ mats, int Np, int k, const double
 #pragma unroll
     for (int r = 0; r < 16; ++r) Uk[stile][srow + 4 * r][scc] = pa[r];
     __syncthreads();
-    // (unconditional -- the last step reloads its own rows: with a branch the
-    // waitcnt pass merges the two paths and makes the MFMAs below wait for the
-    // first prefetched load too; the empty asm keeps the compiler from sinking
-    // the prefetch to its use in the next step, where its latency would be
-    // exposed again)
-    aload(min(p + 1, k - 1));
-    asm volatile("" ::: "memory");
+    // (measured round 4: forcing a true one-step-ahead prefetch here -- an
+    // unconditional load pinned by an empty asm -- ran C5 at 89.9 instead of
+    // 83.6 ms; as written the compiler issues it with the next step's loads)
+    if (p + 1 < k) aload(p + 1);
 #pragma unroll
     for (int ts = 0; ts < DCB / 4; ++ts) {
 #pragma unroll
