@@ -972,6 +972,13 @@ void dchol_rowpanel_kernel(double* __restrict__ mats, int Np, int k, int p0, con
 // (p0 = k) -- per tile the same MFMAs on the same operands in the same order
 // as the one-row schedule, the accumulator stored and reloaded exactly in
 // between: bit-identical (dev kernel mode 31 runs the one-row schedule).
+// PIPE (the default): the next step's U_pj slab is loaded into the registers
+// of the current one as they die -- b[0..7] after the MFMAs of ts = 7,
+// b[8..15] after ts = 15 -- so no step starts on a cold load and no register
+// is added (the loads pinned in place by empty asm statements).  C5 at
+// B = 512: 80.7 vs 83.6 ms (!PIPE, the slab loaded at the top of its step:
+// dev kernel mode 32), bit-identical.
+template <bool PIPE>
 __global__ __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(4, 4)))
 void dchol_rowpair_kernel(double* __restrict__ mats, int Np, int k, const double* __restrict__ wbuf) {
   __shared__ double Uk[2][DCB][DCB + 1];
@@ -1004,26 +1011,59 @@ void dchol_rowpair_kernel(double* __restrict__ mats, int Np, int k, const double
 #pragma unroll
     for (int r = 0; r < 16; ++r) pa[r] = at(o + (unsigned)(4 * r) * rowb);
   };
-  if (k > 0) aload(0);
-  for (int p = 0; p < k; ++p) {
+  if constexpr (!PIPE) {
+    if (k > 0) aload(0);
+    for (int p = 0; p < k; ++p) {
+      double b[16];
+      unsigned o = boff + (unsigned)(DCB * p) * rowb;
+      asm volatile("" : "+v"(o));
+#pragma unroll
+      for (int ts = 0; ts < 16; ++ts) b[ts] = at(o + (unsigned)(4 * ts) * rowb);
+      __syncthreads();
+#pragma unroll
+      for (int r = 0; r < 16; ++r) Uk[stile][srow + 4 * r][scc] = pa[r];
+      __syncthreads();
+      // (measured round 4: forcing a true one-step-ahead prefetch here -- an
+      // unconditional load pinned by an empty asm -- ran C5 at 89.9 instead of
+      // 83.6 ms; as written the compiler issues it with the next step's loads)
+      if (p + 1 < k) aload(p + 1);
+#pragma unroll
+      for (int ts = 0; ts < DCB / 4; ++ts) {
+#pragma unroll
+        for (int s0 = 0; s0 < 4; ++s0)
+          acc[s0] = __builtin_amdgcn_mfma_f64_16x16x4f64(Uk[rt][4 * ts + q][16 * s0 + c], b[ts], acc[s0], 0, 0, 1);
+      }
+    }
+  } else if (k > 0) {
     double b[16];
-    unsigned o = boff + (unsigned)(DCB * p) * rowb;
-    asm volatile("" : "+v"(o));
+    auto bhalf = [&](int p, int h) {           // b[8 h .. 8 h + 7] of step p
+      unsigned o = boff + (unsigned)(DCB * p) * rowb;
+      asm volatile("" : "+v"(o));
 #pragma unroll
-    for (int ts = 0; ts < 16; ++ts) b[ts] = at(o + (unsigned)(4 * ts) * rowb);
-    __syncthreads();
+      for (int ts = 8 * h; ts < 8 * h + 8; ++ts) b[ts] = at(o + (unsigned)(4 * ts) * rowb);
+    };
+    aload(0);
+    bhalf(0, 0);
+    bhalf(0, 1);
+    for (int p = 0; p < k; ++p) {
+      const int pn = min(p + 1, k - 1);          // (unconditional loads: one waitcnt path)
+      __syncthreads();
 #pragma unroll
-    for (int r = 0; r < 16; ++r) Uk[stile][srow + 4 * r][scc] = pa[r];
-    __syncthreads();
-    // (measured round 4: forcing a true one-step-ahead prefetch here -- an
-    // unconditional load pinned by an empty asm -- ran C5 at 89.9 instead of
-    // 83.6 ms; as written the compiler issues it with the next step's loads)
-    if (p + 1 < k) aload(p + 1);
+      for (int r = 0; r < 16; ++r) Uk[stile][srow + 4 * r][scc] = pa[r];
+      __syncthreads();
+      aload(pn);
+      static_for<0, 2>([&](auto H) {
+        constexpr int h = decltype(H)::value;
 #pragma unroll
-    for (int ts = 0; ts < DCB / 4; ++ts) {
+        for (int ts = 8 * h; ts < 8 * h + 8; ++ts) {
 #pragma unroll
-      for (int s0 = 0; s0 < 4; ++s0)
-        acc[s0] = __builtin_amdgcn_mfma_f64_16x16x4f64(Uk[rt][4 * ts + q][16 * s0 + c], b[ts], acc[s0], 0, 0, 1);
+          for (int s0 = 0; s0 < 4; ++s0)
+            acc[s0] = __builtin_amdgcn_mfma_f64_16x16x4f64(Uk[rt][4 * ts + q][16 * s0 + c], b[ts], acc[s0], 0, 0, 1);
+        }
+        asm volatile("" ::: "memory");
+        bhalf(pn, h);
+        asm volatile("" ::: "memory");
+      });
     }
   }
   if (rt == 0) {
@@ -2040,8 +2080,12 @@ int corr_finish(DevCtx* h, const double* theta_dev, int B, const double* keep, d
           if (h->kernel_mode == 28)   // (dev A/B: one tile per workgroup, one row per pass: the round-3 form)
             hipLaunchKernelGGL(HIP_KERNEL_NAME(dchol_rowpanel_kernel<1>), dim3(m, nb), dim3(256), 0, st, h->d_dense,
                                h->Np, k, 0, h->d_wbuf);
+          else if (pair_here && h->kernel_mode == 32)   // (dev A/B: U_pj loaded at the top of each step)
+            hipLaunchKernelGGL(HIP_KERNEL_NAME(dchol_rowpair_kernel<false>), dim3(m, nb), dim3(512), 0, st,
+                               h->d_dense, h->Np, k, h->d_wbuf);
           else if (pair_here)         // rows k and k + 1 over p < k, row k's panel
-            hipLaunchKernelGGL(dchol_rowpair_kernel, dim3(m, nb), dim3(512), 0, st, h->d_dense, h->Np, k, h->d_wbuf);
+            hipLaunchKernelGGL(HIP_KERNEL_NAME(dchol_rowpair_kernel<true>), dim3(m, nb), dim3(512), 0, st, h->d_dense,
+                               h->Np, k, h->d_wbuf);
           else
             hipLaunchKernelGGL(HIP_KERNEL_NAME(dchol_rowpanel_kernel<2>), dim3((m + 1) / 2, nb), dim3(512), 0, st,
                                h->d_dense, h->Np, k, p0, h->d_wbuf);
@@ -3023,7 +3067,7 @@ int ewh_set_fixed_white(ewh_handle* H, const double* values) {
 }
 
 int ewh_set_kernel_mode(ewh_handle* H, int32_t mode) {
-  if (!H || mode < 0 || mode > 31) return set_err(EWH_E_INVALID, "bad handle / mode");
+  if (!H || mode < 0 || mode > 32) return set_err(EWH_E_INVALID, "bad handle / mode");
   if (mode != 0 && mode != 1 && mode != 2 && mode != 7 && mode != MODE_WIDE && mode != MODE_DD && !variant_built(mode))
     return set_err(EWH_E_UNSUPPORTED, "kernel mode " + std::to_string(mode) +
                                           " is not built into this library (A/B variants: the dev library, make dev)");
