@@ -826,47 +826,71 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(4, 4)))
 void dchol_rowupdate2_kernel(double* __restrict__ mats, int Np, int i, int p0) {
   __shared__ double Uj[DCB][DCB + 1];
   const int j = i + blockIdx.x, bl = blockIdx.y, t = threadIdx.x;
-  double* base = mats + (long long)bl * Np * Np;
-  double* Aij = base + (long long)(DCB * i) * Np + DCB * j;
   const int w = t >> 6, lane = t & 63, q = lane >> 4, c = lane & 15;
+  // accesses as the sample's uniform base + 32-bit byte offsets (see
+  // dchol_rowpair_kernel)
+  char* cb = (char*)(mats + (long long)bl * Np * Np);
+  auto at = [&](unsigned off) -> double& { return *(double*)(cb + off); };
+  const unsigned rowb = 8u * (unsigned)Np;
+  const unsigned toff = (unsigned)(DCB * i + 16 * w + q) * rowb + 8u * (unsigned)(DCB * j + c);
   v4d acc[4];
 #pragma unroll
   for (int jb = 0; jb < 4; ++jb)
 #pragma unroll
-    for (int r = 0; r < 4; ++r) acc[jb][r] = Aij[(long long)(16 * w + q + 4 * r) * Np + 16 * jb + c];
-  // A slab of U_pi (column block 16w..16w+15, all 64 rows): loaded at the top
-  // of step p, in flight across the LDS store and barriers; U_pj prefetched
-  // one step ahead into registers for the LDS store
-  const double* acol = base + DCB * i + 16 * w + c + (long long)q * Np;
-  const double* bcol = base + DCB * j + (t & 63) + (long long)(t >> 6) * Np;
+    for (int r = 0; r < 4; ++r) acc[jb][r] = at(toff + (unsigned)(4 * r) * rowb + 8u * (unsigned)(16 * jb));
+  // A slab of U_pi (column block 16w..16w+15, all 64 rows) in registers, U_pj
+  // staged through LDS (prefetched one step ahead into registers)
+  const unsigned aoff = (unsigned)q * rowb + 8u * (unsigned)(DCB * i + 16 * w + c);
+  const unsigned boff = (unsigned)(t >> 6) * rowb + 8u * (unsigned)(DCB * j + (t & 63));
   double pb[16];
   auto bload = [&](int p) {
-    const double* rp = bcol + (long long)(DCB * p) * Np;
+    unsigned o = boff + (unsigned)(DCB * p) * rowb;
+    asm volatile("" : "+v"(o));
 #pragma unroll
-    for (int r = 0; r < 16; ++r) pb[r] = rp[(long long)(4 * r) * Np];
+    for (int r = 0; r < 16; ++r) pb[r] = at(o + (unsigned)(4 * r) * rowb);
   };
-  if (p0 < i) bload(p0);
-  for (int p = p0; p < i; ++p) {
+  // the A slab of the next step is loaded into the registers of this one as
+  // they die (a[0..7] after the MFMAs of ts = 7, a[8..15] after ts = 15), as
+  // in dchol_rowpair_kernel<PIPE>; loads unconditional (the last step reloads
+  // its own rows) so the waitcnt pass sees one path
+  if (p0 < i) {
     double a[16];
-    const double* ap = acol + (long long)(DCB * p) * Np;
+    auto ahalf = [&](int p, int h) {
+      unsigned o = aoff + (unsigned)(DCB * p) * rowb;
+      asm volatile("" : "+v"(o));
 #pragma unroll
-    for (int ts = 0; ts < 16; ++ts) a[ts] = ap[(long long)(4 * ts) * Np];
-    __syncthreads();
+      for (int ts = 8 * h; ts < 8 * h + 8; ++ts) a[ts] = at(o + (unsigned)(4 * ts) * rowb);
+    };
+    bload(p0);
+    ahalf(p0, 0);
+    ahalf(p0, 1);
+    for (int p = p0; p < i; ++p) {
+      const int pn = min(p + 1, i - 1);
+      __syncthreads();
 #pragma unroll
-    for (int r = 0; r < 16; ++r) Uj[(t >> 6) + 4 * r][t & 63] = pb[r];
-    __syncthreads();
-    if (p + 1 < i) bload(p + 1);
+      for (int r = 0; r < 16; ++r) Uj[(t >> 6) + 4 * r][t & 63] = pb[r];
+      __syncthreads();
+      bload(pn);
+      static_for<0, 2>([&](auto H) {
+        constexpr int h = decltype(H)::value;
 #pragma unroll
-    for (int ts = 0; ts < DCB / 4; ++ts) {
+        for (int ts = 8 * h; ts < 8 * h + 8; ++ts) {
 #pragma unroll
-      for (int jb = 0; jb < 4; ++jb)
-        acc[jb] = __builtin_amdgcn_mfma_f64_16x16x4f64(a[ts], Uj[4 * ts + q][16 * jb + c], acc[jb], 0, 0, 1);
+          for (int jb = 0; jb < 4; ++jb)
+            acc[jb] = __builtin_amdgcn_mfma_f64_16x16x4f64(a[ts], Uj[4 * ts + q][16 * jb + c], acc[jb], 0, 0, 1);
+        }
+        asm volatile("" ::: "memory");
+        ahalf(pn, h);
+        asm volatile("" ::: "memory");
+      });
     }
   }
+  unsigned toff2 = toff;
+  asm volatile("" : "+v"(toff2));
 #pragma unroll
   for (int jb = 0; jb < 4; ++jb)
 #pragma unroll
-    for (int r = 0; r < 4; ++r) Aij[(long long)(16 * w + q + 4 * r) * Np + 16 * jb + c] = acc[jb][r];
+    for (int r = 0; r < 4; ++r) at(toff2 + (unsigned)(4 * r) * rowb + 8u * (unsigned)(16 * jb)) = acc[jb][r];
 }
 
 // Row update + panel in one pass for the tiles j > k of block row k (after
