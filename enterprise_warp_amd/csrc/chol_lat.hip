@@ -514,7 +514,11 @@ __device__ __forceinline__ void lat_unit(LatLds<NB>& S, const CholJob* __restric
       if (S.stall) lnl = __builtin_bit_cast(double, LAT_STALL_BITS);
     }
     out_units[(long long)p * B + b] = lnl;
-    host_units[(long long)p * B + b] = lnl;    // pinned: the host folds the P terms after the launch
+    // pinned: the host folds the P terms.  A system-scope store (written
+    // through to host memory at once): a plain store sits in L2 until the
+    // kernel ends, which the persistent server never does between requests
+    __hip_atomic_store(reinterpret_cast<unsigned long long*>(host_units) + (long long)p * B + b,
+                       __builtin_bit_cast(unsigned long long, lnl), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
   }
   LAT_STAMP(12)
 }
