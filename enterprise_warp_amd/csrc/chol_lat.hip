@@ -468,13 +468,14 @@ __device__ __forceinline__ void lat_wave(LatLds<NB>& S, const CholJob& J, const 
   LAT_STAMP(10)
 }
 
-// one unit (pulsar p, sample b) of a latency batch: the whole body of
-// chol_lat_kernel, shared with the persistent chol_lat_server_kernel
 template <int NB, bool STAMP, int VAR>
-__device__ __forceinline__ void lat_unit(LatLds<NB>& S, const CholJob* __restrict__ jobs, int B, int u,
-                                         const double* theta, int ldth, double* __restrict__ out_units,
-                                         double* host_units) {
+__global__ __launch_bounds__(256) void chol_lat_kernel(const CholJob* __restrict__ jobs, int B, int P,
+                                                       const double* theta, int ldth, double* __restrict__ out_units,
+                                                       double* host_units) {
+  __shared__ LatLds<NB> S;
   const int tid = threadIdx.x, w = tid >> 6, lane = tid & 63;
+  (void)P;
+  const int u = blockIdx.x;
   const int p = u / B, b = u % B;
   // theta first: the whole row when it fits the LDS stage, read from pinned
   // host memory before the job record, so its PCIe round trip overlaps the
@@ -514,66 +515,13 @@ __device__ __forceinline__ void lat_unit(LatLds<NB>& S, const CholJob* __restric
       if (S.stall) lnl = __builtin_bit_cast(double, LAT_STALL_BITS);
     }
     out_units[(long long)p * B + b] = lnl;
-    // pinned: the host folds the P terms.  A system-scope store (written
-    // through to host memory at once): a plain store sits in L2 until the
-    // kernel ends, which the persistent server never does between requests
+    // pinned: the host folds the P terms.  A system-scope store, written
+    // through to host memory at once (a plain store can sit in L2 until the
+    // kernel ends; profiles/r04 lat logs)
     __hip_atomic_store(reinterpret_cast<unsigned long long*>(host_units) + (long long)p * B + b,
                        __builtin_bit_cast(unsigned long long, lnl), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
   }
   LAT_STAMP(12)
-}
-
-template <int NB, bool STAMP, int VAR>
-__global__ __launch_bounds__(256) void chol_lat_kernel(const CholJob* __restrict__ jobs, int B, int P,
-                                                       const double* theta, int ldth, double* __restrict__ out_units,
-                                                       double* host_units) {
-  __shared__ LatLds<NB> S;
-  (void)P;
-  lat_unit<NB, STAMP, VAR>(S, jobs, B, (int)blockIdx.x, theta, ldth, out_units, host_units);
-}
-
-// The persistent form (the launch is a third of a B = 1
-// call): one workgroup per unit stays resident and serves request after
-// request from a doorbell in coherent pinned host memory, so a call costs the
-// host's doorbell write, the poll, the unit and the term's write-back -- no
-// kernel launch, no completion signal.  Thread 0 polls (system-scope acquire
-// loads, s_sleep between polls); the workgroup leaves when the host sets
-// `stop`, or when no request came for idle_ticks of the 100 MHz real-time
-// counter -- every wave reaches one of the two, so the grid always drains
-// (the host relaunches a server that may have timed out before it posts).
-// Per request the same lat_unit as chol_lat_kernel: bit-identical terms.
-template <int NB, int VAR>
-__global__ __launch_bounds__(256) void chol_lat_server_kernel(const CholJob* __restrict__ jobs, int B,
-                                                              const double* theta, int ldth,
-                                                              double* __restrict__ out_units, double* host_units,
-                                                              const LatBell* bell, unsigned long long seq0,
-                                                              long long idle_ticks) {
-  __shared__ LatLds<NB> S;
-  __shared__ int cmd;
-  unsigned long long seen = seq0;
-  for (;;) {
-    if (threadIdx.x == 0) {
-      const long long t0 = (long long)__builtin_amdgcn_s_memrealtime();
-      int go = 0;
-      for (;;) {
-        if (__hip_atomic_load(&bell->stop, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM)) break;
-        const unsigned long long sq = __hip_atomic_load(&bell->seq, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_SYSTEM);
-        if (sq != seen) {
-          seen = sq;
-          go = 1;
-          break;
-        }
-        if ((long long)__builtin_amdgcn_s_memrealtime() - t0 > idle_ticks) break;
-        __builtin_amdgcn_s_sleep(1);
-      }
-      cmd = go;
-    }
-    __syncthreads();
-    if (!cmd) return;
-    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "");     // (system scope: theta, written before the doorbell)
-    lat_unit<NB, false, VAR>(S, jobs, B, (int)blockIdx.x, theta, ldth, out_units, host_units);
-    __syncthreads();                                // (LDS and cmd reused by the next request)
-  }
 }
 
 template <bool STAMP, int VAR>
@@ -596,25 +544,6 @@ int launch_chol_lat_t(int nb, const CholJob* jobs, int B, int P, const double* t
 }
 
 }  // namespace
-
-int launch_chol_lat_server(int nb, const CholJob* jobs, int B, int P, const double* theta, int ldth, double* units,
-                           double* host_units, const LatBell* bell, unsigned long long seq0, long long idle_ticks,
-                           hipStream_t st) {
-  const dim3 grid((unsigned)(P * B)), block(256);
-#define EWH_LAT_CASE(N)                                                                                      \
-  case N:                                                                                                    \
-    hipLaunchKernelGGL(HIP_KERNEL_NAME(chol_lat_server_kernel<N, LAT_VAR_FLOW>), grid, block, 0, st, jobs, B, \
-                       theta, ldth, units, host_units, bell, seq0, idle_ticks);                              \
-    break;
-  switch (nb) {
-    EWH_LAT_CASE(1) EWH_LAT_CASE(2) EWH_LAT_CASE(3) EWH_LAT_CASE(4)
-    EWH_LAT_CASE(5) EWH_LAT_CASE(6) EWH_LAT_CASE(7) EWH_LAT_CASE(8)
-    default: return 1;
-  }
-#undef EWH_LAT_CASE
-  const hipError_t e = hipGetLastError();
-  return e == hipSuccess ? 0 : set_err(EWH_E_HIP, std::string("chol_lat_server_kernel: ") + hipGetErrorString(e));
-}
 
 int launch_chol_lat(int nb, const CholJob* jobs, int B, int P, const double* theta, int ldth, double* units,
                     double* host_units, hipStream_t st, bool stamp, int var) {

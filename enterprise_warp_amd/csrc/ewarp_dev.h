@@ -1427,15 +1427,6 @@ constexpr int LAT_NB_MAX = 8;
 // unit term of a latency-kernel unit whose dataflow wait ran out (a NaN
 // payload no other path writes; ewh_lnl_batch returns EWH_E_HIP on it)
 constexpr unsigned long long LAT_STALL_BITS = 0x7ff4dead057a1100ull;
-// the persistent latency server's doorbell (coherent pinned host memory)
-struct LatBell {
-  unsigned long long seq;    // request number, written by the host after theta
-  unsigned int stop;         // 1: every workgroup leaves
-  unsigned int pad;
-};
-int launch_chol_lat_server(int nb, const CholJob* jobs, int B, int P, const double* theta, int ldth, double* units,
-                           double* host_units, const LatBell* bell, unsigned long long seq0, long long idle_ticks,
-                           hipStream_t st);
 int launch_chol_lat(int nb, const CholJob* jobs, int B, int P, const double* theta, int ldth, double* units,
                     double* host_units, hipStream_t st, bool stamp = false, int var = 0);
 // any width (chol_wide.hip): units [u0, u0 + n), slabs of at most cap

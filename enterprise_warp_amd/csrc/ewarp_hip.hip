@@ -27,11 +27,8 @@
 #include "ewarp_dev.h"
 #include "ewarp_desc.h"
 
-#include <algorithm>
 #include <atomic>
 #include <chrono>
-#include <cstdlib>
-#include <mutex>
 #include <map>
 
 namespace ewh_dev {
@@ -2672,18 +2669,6 @@ struct ewh_handle {
   // contexts with peer access to the first one
   long long h2d_bytes = 0;
   long long peer_mask = 1;
-  // the persistent latency server (chol_lat_server_kernel): its own stream and
-  // coherent pinned doorbell / theta rows / unit terms, allocated once and
-  // never reallocated while it runs
-  LatBell* srv_bell = nullptr;
-  LatBell* srv_bell_d = nullptr;
-  double *srv_th = nullptr, *srv_th_d = nullptr;
-  double *srv_units = nullptr, *srv_units_d = nullptr;
-  hipStream_t srv_st = nullptr;
-  bool srv_running = false;
-  int srv_B = 0;
-  unsigned long long srv_seq = 0;
-  std::chrono::steady_clock::time_point srv_last;
 };
 
 namespace {
@@ -2706,76 +2691,6 @@ int ensure_pinned(double** p, size_t* cap, size_t need, const double** cached = 
 }
 
 }  // namespace
-
-// ---- the persistent latency server ----
-// A server workgroup leaves after LAT_SRV_IDLE_TICKS of the 100 MHz real-time
-// counter without a request; the host treats a server it has not used for
-// LAT_SRV_HOST_IDLE (half that) as possibly gone and replaces it before
-// posting, so a request is never posted to a server that may be leaving.
-constexpr long long LAT_SRV_IDLE_TICKS = 2000000;                 // 20 ms
-constexpr auto LAT_SRV_HOST_IDLE = std::chrono::milliseconds(10);
-// batches of the latency path served by the persistent kernel (dev kernel
-// mode 33 forces it; the launch-per-call kernel otherwise)
-constexpr bool LAT_SERVER_DEFAULT = false;
-constexpr int LAT_B_MAX_SRV = 8;      // (= LAT_B_MAX: the latency path's batch bound)
-
-std::mutex g_srv_mu;
-std::vector<ewh_handle*> g_srv_live;   // handles with a server running (stopped at exit)
-
-void lat_server_stop(ewh_handle* H) {
-  if (!H || !H->srv_running) return;
-  (void)hipSetDevice(H->ctx[0]->device);
-  __atomic_store_n(&H->srv_bell->stop, 1u, __ATOMIC_RELEASE);
-  (void)hipStreamSynchronize(H->srv_st);
-  __atomic_store_n(&H->srv_bell->stop, 0u, __ATOMIC_RELEASE);
-  H->srv_running = false;
-  std::lock_guard<std::mutex> lk(g_srv_mu);
-  g_srv_live.erase(std::remove(g_srv_live.begin(), g_srv_live.end(), H), g_srv_live.end());
-}
-
-// at process exit: every server leaves before the runtime (and the pinned
-// doorbell it polls) goes away
-void lat_server_stop_all() {
-  std::vector<ewh_handle*> v;
-  {
-    std::lock_guard<std::mutex> lk(g_srv_mu);
-    v = g_srv_live;
-  }
-  for (ewh_handle* H : v) lat_server_stop(H);
-}
-
-int lat_server_alloc(ewh_handle* H) {
-  if (H->srv_bell) return 0;
-  const unsigned fl = hipHostMallocPortable | hipHostMallocMapped | hipHostMallocCoherent;
-  const size_t nth = (size_t)LAT_B_MAX_SRV * std::max(1, H->n_param), nu = (size_t)H->P * LAT_B_MAX_SRV;
-  hipError_t e = hipHostMalloc((void**)&H->srv_bell, sizeof(LatBell), fl);
-  if (e == hipSuccess) e = hipHostMalloc((void**)&H->srv_th, nth * sizeof(double), fl);
-  if (e == hipSuccess) e = hipHostMalloc((void**)&H->srv_units, nu * sizeof(double), fl);
-  if (e != hipSuccess) return set_err(EWH_E_NOMEM, std::string("hipHostMalloc: ") + hipGetErrorString(e));
-  H->srv_bell->seq = 0;
-  H->srv_bell->stop = 0;
-  EWH_HIP(hipHostGetDevicePointer((void**)&H->srv_bell_d, H->srv_bell, 0));
-  EWH_HIP(hipHostGetDevicePointer((void**)&H->srv_th_d, H->srv_th, 0));
-  EWH_HIP(hipHostGetDevicePointer((void**)&H->srv_units_d, H->srv_units, 0));
-  EWH_HIP(hipStreamCreateWithFlags(&H->srv_st, hipStreamNonBlocking));
-  static bool registered = false;
-  if (!registered) {
-    registered = true;
-    std::atexit(lat_server_stop_all);
-  }
-  return 0;
-}
-
-void lat_server_free(ewh_handle* H) {
-  lat_server_stop(H);
-  if (H->srv_st) (void)hipStreamDestroy(H->srv_st);
-  if (H->srv_bell) (void)hipHostFree(H->srv_bell);
-  if (H->srv_th) (void)hipHostFree(H->srv_th);
-  if (H->srv_units) (void)hipHostFree(H->srv_units);
-  H->srv_st = nullptr;
-  H->srv_bell = nullptr;
-  H->srv_th = H->srv_units = nullptr;
-}
 
 namespace {
 
@@ -2948,92 +2863,11 @@ int lnl_batch_corr_pulsars(ewh_handle* H, int B, double* out_host) {
 constexpr uint64_t LAT_SENTINEL = 0x7ff4dead0ebeef01ull;   // a NaN no kernel writes
 constexpr int LAT_B_MAX = 8;    // batches up to this size take the latency kernel (profiles/r03c/latency.log: B = 16 is faster batched)
 
-// The latency path through the persistent server: theta into its pinned
-// rows, the doorbell, the host spins on the unit terms (as the launch form)
-int lat_server_call(ewh_handle* H, DevCtx* h, int B, double* out_host) {
-  int rc;
-  if ((rc = lat_server_alloc(H)) || (rc = ensure_units(h, B))) return rc;
-  const int np = H->n_param;
-  const size_t nu = (size_t)h->P * B;
-  const auto now = std::chrono::steady_clock::now();
-  if (H->srv_running &&
-      (B != H->srv_B || now - H->srv_last > LAT_SRV_HOST_IDLE || hipStreamQuery(H->srv_st) != hipErrorNotReady))
-    lat_server_stop(H);
-  if (np > 0) std::memcpy(H->srv_th, H->h_theta, sizeof(double) * (size_t)B * np);
-  volatile uint64_t* hu = reinterpret_cast<volatile uint64_t*>(H->srv_units);
-  for (size_t i = 0; i < nu; ++i) hu[i] = LAT_SENTINEL;
-  auto start = [&](unsigned long long seq0) -> int {
-    int r = launch_chol_lat_server(h->lat_nb, h->d_jobs_fixed, B, h->P, H->srv_th_d, np, h->d_units,
-                                   H->srv_units_d, H->srv_bell_d, seq0, LAT_SRV_IDLE_TICKS, H->srv_st);
-    if (r) return r < 0 ? r : set_err(EWH_E_UNSUPPORTED, "latency server: block count");
-    H->srv_running = true;
-    H->srv_B = B;
-    std::lock_guard<std::mutex> lk(g_srv_mu);
-    g_srv_live.push_back(H);
-    return 0;
-  };
-  if (!H->srv_running && (rc = start(H->srv_seq))) return rc;
-  std::atomic_thread_fence(std::memory_order_release);
-  __atomic_store_n(&H->srv_bell->seq, ++H->srv_seq, __ATOMIC_RELEASE);
-  const auto t0 = std::chrono::steady_clock::now();
-  size_t seen = 0;
-  bool restarted = false;
-  for (long spins = 0;; ++spins) {
-    while (seen < nu && hu[seen] != LAT_SENTINEL) ++seen;
-    if (seen == nu) break;
-    if ((spins & 4095) == 4095) {
-      const hipError_t q = hipStreamQuery(H->srv_st);
-      if (q != hipSuccess && q != hipErrorNotReady) {
-        H->srv_running = false;
-        return set_err(EWH_E_HIP, std::string("chol_lat_server_kernel: ") + hipGetErrorString(q));
-      }
-      if (q == hipSuccess) {
-        // the server left before this request (never expected: the host
-        // replaces an idle one first); start one on the posted request, once
-        for (seen = 0; seen < nu && hu[seen] != LAT_SENTINEL; ++seen) {
-        }
-        if (seen == nu) break;
-        lat_server_stop(H);
-        if (restarted) return set_err(EWH_E_HIP, "latency server: the request was not served");
-        restarted = true;
-        if ((rc = start(H->srv_seq - 1))) return rc;
-      }
-      if (std::chrono::steady_clock::now() - t0 > std::chrono::seconds(2)) {
-        lat_server_stop(H);
-        for (seen = 0; seen < nu && hu[seen] != LAT_SENTINEL; ++seen) {
-        }
-        if (seen != nu) return set_err(EWH_E_HIP, "latency server: unit terms missing");
-        break;
-      }
-    }
-  }
-  std::atomic_thread_fence(std::memory_order_acquire);
-  for (size_t i = 0; i < nu; ++i)
-    if (hu[i] == LAT_STALL_BITS) {
-      lat_server_stop(H);
-      return set_err(EWH_E_HIP, "chol_lat_server_kernel: a dataflow wait of unit " + std::to_string(i) +
-                                    " ran out (LAT_SPIN_MAX); no lnL was produced");
-    }
-  for (int b = 0; b < B; ++b) {
-    double sum = 0.0;
-    for (int p = 0; p < h->P; ++p) sum += H->srv_units[(size_t)p * B + b];
-    out_host[b] = sum;
-  }
-  H->srv_last = std::chrono::steady_clock::now();
-  H->last_split.assign(1, {0, (long long)H->P * B});
-  H->last_B = B;
-  h->last_B = B;
-  return 0;
-}
-
 int lnl_batch_single(ewh_handle* H, DevCtx* h, int B, double* out_host) {
   int rc;
   EWH_HIP(hipSetDevice(h->device));
-  const int km = h->kernel_mode;
-  if (h->lat_nb > 0 && B <= LAT_B_MAX && (km == 33 || (km == 0 && LAT_SERVER_DEFAULT)))
-    return lat_server_call(H, h, B, out_host);
-  lat_server_stop(H);
   if ((rc = ensure_pinned(&H->h_out, &H->h_out_cap, (size_t)B, &H->lat_out_host))) return rc;
+  const int km = h->kernel_mode;
   if (h->lat_nb > 0 && B <= LAT_B_MAX && (km == 0 || km == 22 || km == 23 || km == 24 || km == 25)) {
     // latency path: one launch reads theta from the pinned staging and writes
     // the unit terms to pinned memory (chol_lat.hip); the host folds them
@@ -3234,7 +3068,6 @@ int ewh_transfer_stats(const ewh_handle* H, int64_t* h2d_bytes, int64_t* peer) {
 int ewh_num_devices(const ewh_handle* H) { return H ? (int)H->ctx.size() : 0; }
 
 int ewh_set_fixed_white(ewh_handle* H, const double* values) {
-  lat_server_stop(H);
   if (!H || !values) return set_err(EWH_E_INVALID, "bad arguments");
   for (DevCtx* h : H->ctx) {
     EWH_HIP(hipSetDevice(h->device));
@@ -3258,8 +3091,7 @@ int ewh_set_fixed_white(ewh_handle* H, const double* values) {
 }
 
 int ewh_set_kernel_mode(ewh_handle* H, int32_t mode) {
-  if (!H || mode < 0 || mode > 33) return set_err(EWH_E_INVALID, "bad handle / mode");
-  lat_server_stop(H);
+  if (!H || mode < 0 || mode > 32) return set_err(EWH_E_INVALID, "bad handle / mode");
   if (mode != 0 && mode != 1 && mode != 2 && mode != 7 && mode != MODE_WIDE && mode != MODE_DD && !variant_built(mode))
     return set_err(EWH_E_UNSUPPORTED, "kernel mode " + std::to_string(mode) +
                                           " is not built into this library (A/B variants: the dev library, make dev)");
@@ -3287,7 +3119,6 @@ double ewh_unit_cost(const ewh_handle* H, int32_t p) {
 int ewh_lnl_units_device(ewh_handle* H, const double* theta_dev, int32_t B, int64_t u_begin, int64_t u_end,
                          double* out_dev, void* stream) {
   if (!H || !theta_dev || !out_dev || B <= 0) return set_err(EWH_E_INVALID, "bad arguments");
-  lat_server_stop(H);
   DevCtx* h = H->ctx[0];
   if (h->osmode) return set_err(EWH_E_UNSUPPORTED, "an optimal-statistic handle evaluates ewh_optstat only");
   int rc = ctx_units(h, theta_dev, B, u_begin, u_end, out_dev, (hipStream_t)stream, true);
@@ -3401,7 +3232,6 @@ int ewh_lnl_batch(ewh_handle* H, const double* theta_host, int32_t B, double* ou
 
 int ewh_contract_device(ewh_handle* H, const double* theta_dev, int32_t B, void* stream) {
   if (!H || !theta_dev || B <= 0) return set_err(EWH_E_INVALID, "bad arguments");
-  lat_server_stop(H);
   DevCtx* h = H->ctx[0];
   if (h->white_fixed || h->corr || h->osmode)
     return set_err(EWH_E_UNSUPPORTED, "ewh_contract_device: white noise must vary (uncorrelated / CURN handle)");
@@ -3426,7 +3256,6 @@ int ewh_corr_partial_device(ewh_handle* H, const double* theta_dev, int32_t B, i
   if (!H || !H->corr || !theta_dev || !keep_dev || !local_dev || B <= 0 || p_begin < 0 || p_end > H->P ||
       p_begin > p_end)
     return set_err(EWH_E_INVALID, "bad arguments (needs a correlated-common-process handle)");
-  lat_server_stop(H);
   DevCtx* h = H->ctx[0];
   EWH_HIP(hipSetDevice(h->device));
   int rc = corr_partial(h, theta_dev, B, p_begin, p_end, local_dev, keep_dev, (hipStream_t)stream);
@@ -3439,7 +3268,6 @@ int ewh_corr_finish_device(ewh_handle* H, const double* theta_dev, int32_t B, co
                            const double* local_dev, double* out_dev, void* stream) {
   if (!H || !H->corr || !theta_dev || !keep_dev || !local_dev || !out_dev || B <= 0)
     return set_err(EWH_E_INVALID, "bad arguments (needs a correlated-common-process handle)");
-  lat_server_stop(H);
   DevCtx* h = H->ctx[0];
   hipStream_t st = (hipStream_t)stream;
   EWH_HIP(hipSetDevice(h->device));
@@ -3458,13 +3286,11 @@ int ewh_corr_finish_device(ewh_handle* H, const double* theta_dev, int32_t B, co
 int ewh_optstat(ewh_handle* H, const double* theta_host, int32_t B, const double* phihat_host, double* rho_host,
                 double* sig_host, double* os_host, double* os_sig_host) {
   if (!H) return set_err(EWH_E_INVALID, "bad arguments");
-  lat_server_stop(H);
   return ctx_optstat(H->ctx[0], theta_host, B, phihat_host, rho_host, sig_host, os_host, os_sig_host);
 }
 
 int ewh_last_unit_terms(ewh_handle* H, double* out_host, int32_t B) {
   if (!H || !out_host || B != H->last_B || H->last_split.empty()) return set_err(EWH_E_INVALID, "no matching previous call");
-  lat_server_stop(H);
   const int P = H->P, nd = (int)H->last_split.size();
   const bool by_samples = nd == 1 ? false : H->corr;
   std::memset(out_host, 0, sizeof(double) * (size_t)P * B);
@@ -3494,7 +3320,6 @@ int ewh_last_unit_terms(ewh_handle* H, double* out_host, int32_t B) {
 
 void ewh_destroy(ewh_handle* H) {
   if (!H) return;
-  lat_server_free(H);
   for (size_t i = 0; i < H->ev.size(); ++i) {
     (void)hipSetDevice(H->ctx[i]->device);
     (void)hipEventDestroy(H->ev[i]);

@@ -1,7 +1,10 @@
 // Probe (dev only, not part of the library): can a running kernel see a flag
-// the host writes into coherent pinned host memory, and how fast?  The
-// persistent latency server (chol_lat.hip, kernel mode 33) polls its doorbell
-// this way and on the first GPU run never saw a request while it ran.  One
+// the host writes into coherent pinned host memory, and how fast?  Written for
+// the round-4 persistent latency server experiment (measured
+// slower than a launch per call, removed).  Result (MI355X): a system-scope
+// atomic load, a volatile load and a fenced relaxed load all see the flag
+// within one poll (~1.4 us per poll, a PCIe round trip); a nontemporal load
+// never does.  One
 // wave polls a host flag with one of several load forms until it reads 1 or
 // 50 ms of the 100 MHz real-time counter pass (every poll loop is bounded);
 // the host sets the flag 2 ms after the launch.  Prints, per form and
