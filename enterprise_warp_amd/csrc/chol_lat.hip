@@ -58,12 +58,9 @@ constexpr unsigned char LAT_MAP[9][8][8] = {{},
 // LAT_VAR_STALL (dev test only): LAT_VAR_FLOW with every wait running out at
 // once, so the stall path (LAT_STALL_BITS -> an error of ewh_lnl_batch) is
 // exercised (tests/test_gpu_properties.py).
-// LAT_VAR_PLAIN (dev A/B): LAT_VAR_FLOW with the unit term stored to the
-// pinned buffer by a plain store instead of a system-scope one.
-[[maybe_unused]] constexpr int LAT_VAR_FLOW = 0, LAT_VAR_BARRIER = 1, LAT_VAR_R3 = 2, LAT_VAR_STALL = 3,
-                               LAT_VAR_PLAIN = 4;
+[[maybe_unused]] constexpr int LAT_VAR_FLOW = 0, LAT_VAR_BARRIER = 1, LAT_VAR_R3 = 2, LAT_VAR_STALL = 3;
 constexpr bool lat_pre(int var) { return var != LAT_VAR_R3; }
-constexpr bool lat_is_flow(int var) { return var == LAT_VAR_FLOW || var == LAT_VAR_STALL || var == LAT_VAR_PLAIN; }
+constexpr bool lat_is_flow(int var) { return var == LAT_VAR_FLOW || var == LAT_VAR_STALL; }
 template <int NB, int VAR>
 constexpr int lat_owner(int i, int j) { return VAR == LAT_VAR_R3 ? (i + j) & 3 : LAT_MAP[NB][i][j]; }
 // wave w owns a block (bb, j > bb) of block row bb
@@ -518,14 +515,10 @@ __global__ __launch_bounds__(256) void chol_lat_kernel(const CholJob* __restrict
       if (S.stall) lnl = __builtin_bit_cast(double, LAT_STALL_BITS);
     }
     out_units[(long long)p * B + b] = lnl;
-    // pinned: the host folds the P terms.  A system-scope store, written
-    // through to host memory at once (a plain store can sit in L2 until the
-    // kernel ends; profiles/r04 lat logs)
-    if constexpr (VAR == LAT_VAR_PLAIN)
-      host_units[(long long)p * B + b] = lnl;
-    else
-      __hip_atomic_store(reinterpret_cast<unsigned long long*>(host_units) + (long long)p * B + b,
-                         __builtin_bit_cast(unsigned long long, lnl), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+    // pinned: the host folds the P terms after the launch.  (A system-scope
+    // store, written through at once, measured the same at B = 1 and slower at
+    // B = 8: 29.50 / 37.5 vs 29.48 / 35.9 us, round 4.)
+    host_units[(long long)p * B + b] = lnl;
   }
   LAT_STAMP(12)
 }
@@ -560,8 +553,6 @@ int launch_chol_lat(int nb, const CholJob* jobs, int B, int P, const double* the
   if (var == LAT_VAR_R3) return launch_chol_lat_t<false, LAT_VAR_R3>(nb, jobs, B, P, theta, ldth, units, host_units, st);
   if (var == LAT_VAR_STALL)
     return launch_chol_lat_t<false, LAT_VAR_STALL>(nb, jobs, B, P, theta, ldth, units, host_units, st);
-  if (var == LAT_VAR_PLAIN)
-    return launch_chol_lat_t<false, LAT_VAR_PLAIN>(nb, jobs, B, P, theta, ldth, units, host_units, st);
 #endif
   (void)stamp;
   (void)var;

@@ -2868,7 +2868,7 @@ int lnl_batch_single(ewh_handle* H, DevCtx* h, int B, double* out_host) {
   EWH_HIP(hipSetDevice(h->device));
   if ((rc = ensure_pinned(&H->h_out, &H->h_out_cap, (size_t)B, &H->lat_out_host))) return rc;
   const int km = h->kernel_mode;
-  if (h->lat_nb > 0 && B <= LAT_B_MAX && (km == 0 || km == 22 || km == 23 || km == 24 || km == 25 || km == 33)) {
+  if (h->lat_nb > 0 && B <= LAT_B_MAX && (km == 0 || km == 22 || km == 23 || km == 24 || km == 25)) {
     // latency path: one launch reads theta from the pinned staging and writes
     // the unit terms to pinned memory (chol_lat.hip); the host folds them
     if ((rc = ensure_units(h, B)) || (rc = ensure_pinned(&H->h_out, &H->h_out_cap, (size_t)h->P * B, &H->lat_out_host))) return rc;
@@ -2892,7 +2892,7 @@ int lnl_batch_single(ewh_handle* H, DevCtx* h, int B, double* out_host) {
     volatile uint64_t* hu = reinterpret_cast<volatile uint64_t*>(H->h_out);
     for (size_t i = 0; i < nu; ++i) hu[i] = LAT_SENTINEL;
     if ((rc = launch_chol_lat(h->lat_nb, h->d_jobs_fixed, B, h->P, th_dev, h->n_param, h->d_units, out_dev,
-                              h->stream, km == 22, km == 24 ? 1 : km == 25 ? 2 : km == 23 ? 3 : km == 33 ? 4 : 0)) < 0)
+                              h->stream, km == 22, km == 24 ? 1 : km == 25 ? 2 : km == 23 ? 3 : 0)) < 0)
       return rc;
     if (rc == 0) {
       const auto t0 = std::chrono::steady_clock::now();
@@ -3091,7 +3091,7 @@ int ewh_set_fixed_white(ewh_handle* H, const double* values) {
 }
 
 int ewh_set_kernel_mode(ewh_handle* H, int32_t mode) {
-  if (!H || mode < 0 || mode > 33) return set_err(EWH_E_INVALID, "bad handle / mode");
+  if (!H || mode < 0 || mode > 32) return set_err(EWH_E_INVALID, "bad handle / mode");
   if (mode != 0 && mode != 1 && mode != 2 && mode != 7 && mode != MODE_WIDE && mode != MODE_DD && !variant_built(mode))
     return set_err(EWH_E_UNSUPPORTED, "kernel mode " + std::to_string(mode) +
                                           " is not built into this library (A/B variants: the dev library, make dev)");
