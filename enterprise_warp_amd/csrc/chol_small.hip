@@ -20,7 +20,7 @@ void launch_chol_mfma(const CholJob* jobs, int B, long long u0, long long n, int
 // 24, 25: latency-kernel variants, chol_lat.hip LAT_VAR_BARRIER / LAT_VAR_R3;
 // 26: one wave per SIMD, whole triangle resident, plain right-looking order;
 // 28: the C5 row update + panel with one tile per workgroup, one block row
-// per pass (round 3); 30: the compensated contraction at every width;
+// per pass (round 3); 30: the TwoSum contraction up to 10 blocks;
 // 31: the C5 row update one block row per pass, two tiles per workgroup;
 // 32: the C5 pair kernel with each U_pj slab loaded at the top of its step)
 bool variant_built(int mode) {

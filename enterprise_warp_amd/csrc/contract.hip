@@ -165,22 +165,23 @@ template <int NB>
 int launch_contract2(int waves, const PsrDev& P, const double* w, const double* beta, double* s, long long s_stride,
                      double* G, int nb_samples, hipStream_t st) {
   // (the dynamic-LDS attribute is set per device by set_contract_attributes)
-  constexpr int SP = contract2_split(NB);
-  constexpr bool CP = contract2_comp(NB);
+  constexpr int CP = contract2_comp(NB);
 #ifdef EWH_DEV
-  if (waves == 30 && !CP) {   // (dev A/B: the compensated sum below contract2_comp's width)
-    hipLaunchKernelGGL(HIP_KERNEL_NAME(contract2_kernel<NB, 8, SP, true>), dim3(nb_samples, SP), dim3(512),
-                       contract2_lds(NB), st, P, w, beta, s, s_stride, G);
-    return 0;
+  if constexpr (NB <= 10) {
+    if (waves == 30) {   // (dev A/B: TwoSum accumulation)
+      hipLaunchKernelGGL(HIP_KERNEL_NAME(contract2_kernel<NB, 8, CT_TWOSUM>), dim3(nb_samples), dim3(512),
+                         contract2_lds(NB), st, P, w, beta, s, s_stride, G);
+      return 0;
+    }
   }
 #endif
   if (waves == 0 || waves == 30) waves = contract2_default_waves(NB);
   if (waves == 8)
-    hipLaunchKernelGGL(HIP_KERNEL_NAME(contract2_kernel<NB, 8, SP, CP>), dim3(nb_samples, SP), dim3(512),
-                       contract2_lds(NB), st, P, w, beta, s, s_stride, G);
+    hipLaunchKernelGGL(HIP_KERNEL_NAME(contract2_kernel<NB, 8, CP>), dim3(nb_samples), dim3(512), contract2_lds(NB),
+                       st, P, w, beta, s, s_stride, G);
   else
-    hipLaunchKernelGGL(HIP_KERNEL_NAME(contract2_kernel<NB, 4, SP, CP>), dim3(nb_samples, SP), dim3(256),
-                       contract2_lds(NB), st, P, w, beta, s, s_stride, G);
+    hipLaunchKernelGGL(HIP_KERNEL_NAME(contract2_kernel<NB, 4, CP>), dim3(nb_samples), dim3(256), contract2_lds(NB),
+                       st, P, w, beta, s, s_stride, G);
   return 0;
 }
 
@@ -196,15 +197,14 @@ int dispatch_contract2(int nb, int waves, const PsrDev& P, const double* w, cons
 
 template <int NB>
 int set_attr2() {
-  constexpr int SP = contract2_split(NB);
-  constexpr bool CP = contract2_comp(NB);
-  EWH_HIP(hipFuncSetAttribute((const void*)contract2_kernel<NB, 4, SP, CP>, hipFuncAttributeMaxDynamicSharedMemorySize,
+  constexpr int CP = contract2_comp(NB);
+  EWH_HIP(hipFuncSetAttribute((const void*)contract2_kernel<NB, 4, CP>, hipFuncAttributeMaxDynamicSharedMemorySize,
                               (int)contract2_lds(NB)));
-  EWH_HIP(hipFuncSetAttribute((const void*)contract2_kernel<NB, 8, SP, CP>, hipFuncAttributeMaxDynamicSharedMemorySize,
+  EWH_HIP(hipFuncSetAttribute((const void*)contract2_kernel<NB, 8, CP>, hipFuncAttributeMaxDynamicSharedMemorySize,
                               (int)contract2_lds(NB)));
 #ifdef EWH_DEV
-  if constexpr (!CP)
-    EWH_HIP(hipFuncSetAttribute((const void*)contract2_kernel<NB, 8, SP, true>,
+  if constexpr (NB <= 10)
+    EWH_HIP(hipFuncSetAttribute((const void*)contract2_kernel<NB, 8, CT_TWOSUM>,
                                 hipFuncAttributeMaxDynamicSharedMemorySize, (int)contract2_lds(NB)));
 #endif
   return 0;

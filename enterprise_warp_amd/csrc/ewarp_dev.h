@@ -228,7 +228,8 @@ __device__ __forceinline__ dd dd_sqrt(dd x) {
 // per-pulsar device tables
 // ----------------------------------------------------------------------------
 constexpr int CT_ROWS = 32;   // TOA rows per contraction tile (8 MFMA k-steps); T_aug is padded by this many zero rows
-constexpr int CT_GROUP = 2;   // contract2: tiles per compensated-accumulation group (a power of two)
+constexpr int CT_GROUP = 2;   // contract2: tiles per accumulation group (a power of two)
+constexpr int CT_SINGLE = 0, CT_BLOCKED = 1, CT_TWOSUM = 2;   // contract2 accumulation forms
 
 struct PsrDev {
   int n_toa, m, ld, nb;      // varying layout: T_aug is n_toa x ld, r at ld-1
@@ -432,7 +433,7 @@ constexpr bool wave_uses(int nb, int wave, int j, int W = 4) {
 // per-tile weights); VW / WS: the virtual wave that picks the output blocks
 // (blocks VW + WS sl) and the virtual waves per sample -- WS = W SPLIT when a
 // sample's blocks are split over SPLIT workgroups (contract2_kernel).
-template <int NB, int WAVE, int W, int VW = WAVE, int WS = W, bool COMP = true>
+template <int NB, int WAVE, int W, int VW = WAVE, int WS = W, int COMP = CT_BLOCKED>
 __device__ __forceinline__ void contract2_body(const PsrDev& P, const double* __restrict__ wrow,
                                                const double* __restrict__ brow, double* __restrict__ srow,
                                                double* __restrict__ Gout) {
@@ -451,14 +452,18 @@ __device__ __forceinline__ void contract2_body(const PsrDev& P, const double* __
   int* const ebase = (int*)(ewbase + 2 * CT_ROWS);
   int* const fmbase = ebase + 2 * CT_ROWS;
 
-  // compensated accumulation: each group of CT_GROUP tiles
+  // blocked accumulation: each group of CT_GROUP tiles
   // (CT_GROUP x 32 TOA rows) is summed by the MFMAs into a fresh accumulator
-  // acc, which is then added into the running sum hi + lo by TwoSum (Knuth:
-  // exact); G = hi + lo at the end.  A single fp64 accumulator over all rows
-  // lost up to ~30x the strict bound of lnL on ill-conditioned prior draws
-  // through the timing-model / red-noise near-degeneracy (tests/golden
-  // c4_small sample 0: 4.0 vs enterprise's 2.3 strict); per group the error
-  // grows only over CT_GROUP x 32 rows.
+  // acc, which is then added into the running sum hi (CT_BLOCKED), or into hi
+  // + lo by TwoSum (CT_TWOSUM, dev A/B); G = hi (+ lo) at the end.  A single
+  // fp64 accumulator over all rows (CT_SINGLE) lost up to ~30x the strict
+  // bound of lnL on ill-conditioned prior draws through the timing-model /
+  // red-noise near-degeneracy (tests/golden c4_small sample 0: 4.0 vs
+  // enterprise's 2.3 strict); per group the error grows only over CT_GROUP x
+  // 32 rows, and the sum of the groups over n / 64 terms (restated on the
+  // host, c4_small prior draws in strict units: single -2.1 / -27 / -8.6,
+  // blocked -1.1 / -4.3 / -0.2, TwoSum -0.9 / 1.2 / 0.3 on samples 0 / 1 / 5,
+  // against enterprise's -2.3 / -195 / -41).
   v4d acc[SLOTS > 0 ? SLOTS : 1], hi[SLOTS > 0 ? SLOTS : 1], lo[SLOTS > 0 ? SLOTS : 1];
 #pragma unroll
   for (int sl = 0; sl < SLOTS; ++sl) {
@@ -467,15 +472,19 @@ __device__ __forceinline__ void contract2_body(const PsrDev& P, const double* __
     lo[sl] = v4d{0.0, 0.0, 0.0, 0.0};
   }
   auto flush = [&]() {
-    if constexpr (!COMP) return;
+    if constexpr (COMP == CT_SINGLE) return;
     static_for<0, SLOTS>([&](auto SL) {
       constexpr int sl = decltype(SL)::value;
       static_for<0, 4>([&](auto R) {
         constexpr int r = decltype(R)::value;
-        const double a = hi[sl][r], b = acc[sl][r];
-        const double sum = a + b, bp = sum - a;
-        lo[sl][r] += (a - (sum - bp)) + (b - bp);
-        hi[sl][r] = sum;
+        if constexpr (COMP == CT_TWOSUM) {
+          const double a = hi[sl][r], b = acc[sl][r];
+          const double sum = a + b, bp = sum - a;
+          lo[sl][r] += (a - (sum - bp)) + (b - bp);
+          hi[sl][r] = sum;
+        } else {
+          hi[sl][r] += acc[sl][r];
+        }
         acc[sl][r] = 0.0;
       });
     });
@@ -613,7 +622,8 @@ __device__ __forceinline__ void contract2_body(const PsrDev& P, const double* __
 #pragma unroll
     for (int r = 0; r < 4; ++r) {
       const int row = 16 * bi + q + 4 * r, col = 16 * bj + c;
-      double v = COMP ? hi[decltype(SL)::value][r] + lo[decltype(SL)::value][r] : acc[decltype(SL)::value][r];
+      constexpr int sl = decltype(SL)::value;
+      double v = COMP == CT_TWOSUM ? hi[sl][r] + lo[sl][r] : COMP == CT_BLOCKED ? hi[sl][r] : acc[sl][r];
       if (row == col && row >= P.m && row < LD - 1) v = 1.0;
       Gout[(long long)row * LD + col] = v;
       Gout[(long long)col * LD + row] = v;
@@ -622,39 +632,31 @@ __device__ __forceinline__ void contract2_body(const PsrDev& P, const double* __
 }
 
 // W = 4 or 8 waves per workgroup (8: half the accumulators per wave, so the
-// narrow NB = 9 kernel fits 2 waves per SIMD).  SPLIT = 2 (wide bases,
-// contract2_split): a sample's output blocks are split over two workgroups
-// (blockIdx.y), each streaming the whole basis, so the three accumulator
-// sets of the compensated sum fit the register budget; each half has its own
-// epoch-sum scratch row (s_stride apart).
-template <int NB, int W, int SPLIT = 1, bool COMP = true>
+// narrow NB = 9 kernel fits 4 waves per SIMD and the wide NB = 13 one 2).
+template <int NB, int W, int COMP = CT_BLOCKED>
 __global__ __launch_bounds__(64 * W) void contract2_kernel(PsrDev P, const double* __restrict__ w,
                                                            const double* __restrict__ beta, double* __restrict__ s,
                                                            long long s_stride, double* __restrict__ G) {
-  constexpr int LD = 16 * NB;
-  const int bl = blockIdx.x, half = SPLIT > 1 ? (int)blockIdx.y : 0;
+  const int bl = blockIdx.x;
   const double* wrow = w + (long long)bl * P.n_toa;
   const double* brow = beta + (long long)bl * P.n_epoch;
-  double* srow = s + ((long long)bl * SPLIT + half) * s_stride;
-  double* Gout = G + (long long)bl * LD * LD;
+  double* srow = s + (long long)bl * s_stride;
+  double* Gout = G + (long long)bl * 16 * NB * 16 * NB;
   const int wv = threadIdx.x >> 6;
-  static_for<0, SPLIT>([&](auto H) {
-    static_for<0, W>([&](auto WV) {
-      constexpr int h = decltype(H)::value, wave = decltype(WV)::value;
-      if (half == h && wv == wave)
-        contract2_body<NB, wave, W, h * W + wave, W * SPLIT, COMP>(P, wrow, brow, srow, Gout);
-    });
+  static_for<0, W>([&](auto WV) {
+    constexpr int wave = decltype(WV)::value;
+    if (wv == wave) contract2_body<NB, wave, W, wave, W, COMP>(P, wrow, brow, srow, Gout);
   });
 }
-// blocks of a sample split over two workgroups from this width on (the
-// compensated accumulators of 8 waves exceed 256 registers above NB = 10)
-constexpr int contract2_split(int nb) { return nb >= 11 ? 2 : 1; }
-// the compensated sum from this width on.  Below it (C2's 9 blocks) the
-// three accumulator sets would halve the occupancy (4 -> 2 waves per SIMD:
-// C2's contraction 18.2 -> 27.3 ms, profiles/r04*), and the single
-// accumulator already meets the per-sample accuracy bound there (c2_small,
-// the C2 bench draws); dev kernel mode 30 compensates every width
-constexpr bool contract2_comp(int nb) { return nb >= 10; }
+// the accumulation per width: blocked from 10 blocks on (C4's 13: the same
+// registers as the single accumulator plus one set -- 2 waves per SIMD as
+// before); below, the single accumulator meets the per-sample accuracy bound
+// (c2_small, the C2 bench draws) and the extra set would halve C2's occupancy
+// (4 -> 2 waves per SIMD).  (Round 4 first used TwoSum at 10+ blocks: three
+// accumulator sets, so 11+ blocks had to split a sample over two workgroups;
+// C4 5.44 k evals/s, vs 6.51 k with one accumulator.)  Dev kernel mode 30:
+// TwoSum at every width up to 10 blocks (A/B).
+constexpr int contract2_comp(int nb) { return nb >= 10 ? CT_BLOCKED : CT_SINGLE; }
 
 // ----------------------------------------------------------------------------
 // batched factorisation, MFMA register-blocked: one wave (64 lanes) per unit.

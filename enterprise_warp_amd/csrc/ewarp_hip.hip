@@ -1725,12 +1725,7 @@ int ensure_var_scratch(DevCtx* h, int B) {
   // contraction's last epoch tile reads zero-initialised pad rows
   const size_t sstride = ((maxe + CT_ROWS - 1) / CT_ROWS + 1) * CT_ROWS * maxld;
   const bool wide = maxld > 16 * BIG_NB_MAX;        // G_lo for the double-double factorisation
-  // epoch-sum rows per sample: two when contract2_kernel splits a sample's
-  // blocks over two workgroups (one row per half)
-  size_t nsrow = 1;
-  for (auto& ps : h->psr)
-    if (ps.dev.n_bgroup == 0 && ps.nb <= CONTRACT2_NB_MAX && contract2_split(ps.nb) > 1) nsrow = 2;
-  const size_t per = ((wide ? 2 : 1) * maxld * maxld + nsrow * sstride + maxn + maxe + maxfac + 1) * sizeof(double);
+  const size_t per = ((wide ? 2 : 1) * maxld * maxld + sstride + maxn + maxe + maxfac + 1) * sizeof(double);
   size_t cap = std::min<size_t>(1024, std::max<size_t>(1, (size_t)1536 * 1024 * 1024 / per));
   // whole rounds of workgroups over the 256 CUs (a chunk of 853 samples of
   // C2 ran 2 rounds of 512 workgroups, the second two-thirds empty)
@@ -1740,8 +1735,8 @@ int ensure_var_scratch(DevCtx* h, int B) {
   int rc;
   if ((rc = dalloc(h, &h->d_w, chunk * maxn))) return rc;
   if ((rc = dalloc(h, &h->d_beta, chunk * maxe))) return rc;
-  if ((rc = dalloc(h, &h->d_s, nsrow * chunk * sstride))) return rc;
-  EWH_HIP(hipMemset(h->d_s, 0, nsrow * chunk * sstride * sizeof(double)));
+  if ((rc = dalloc(h, &h->d_s, chunk * sstride))) return rc;
+  EWH_HIP(hipMemset(h->d_s, 0, chunk * sstride * sizeof(double)));
   h->s_stride = (long long)sstride;
   if ((rc = dalloc(h, &h->d_G, chunk * maxld * maxld))) return rc;
   if ((rc = dalloc(h, &h->d_Kb, chunk))) return rc;
@@ -1769,7 +1764,7 @@ int run_white(DevCtx* h, int p, const double* theta, int ldth, int b0, int nb) {
                      h->d_beta, h->d_Kb, h->d_fac);
   if (ps.dev.n_bgroup == 0 && h->kernel_mode != 7 && ps.nb <= CONTRACT2_NB_MAX) {
     // (dev library A/B: mode 15 = 4 waves per sample, mode 16 = 8)
-    // (30: the compensated sum at every width)
+    // (30: TwoSum accumulation up to 10 blocks)
     const int waves = h->kernel_mode == 15 ? 4 : h->kernel_mode == 16 ? 8 : h->kernel_mode == 30 ? 30 : 0;
     int rc = launch_contract2_nb(ps.nb, waves, ps.dev, h->d_w, h->d_beta, h->d_s, h->s_stride, h->d_G, nb, h->stream);
     if (rc) return rc;
