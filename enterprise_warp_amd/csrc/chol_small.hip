@@ -22,11 +22,10 @@ void launch_chol_mfma(const CholJob* jobs, int B, long long u0, long long n, int
 // 28: the C5 row update + panel with one tile per workgroup, one block row
 // per pass (round 3); 30: the TwoSum contraction up to 10 blocks;
 // 31: the C5 row update one block row per pass, two tiles per workgroup;
-// 32: the C5 pair kernel with each U_pj slab loaded at the top of its step;
-// 34: the C5 pair kernel without the next diagonal tile's pre-update)
+// 32: the C5 pair kernel with each U_pj slab loaded at the top of its step)
 bool variant_built(int mode) {
   return mode == 15 || mode == 16 || mode == 17 || mode == 19 || mode == 21 || mode == 22 || mode == 23 ||
-         mode == 24 || mode == 25 || mode == 26 || mode == 28 || mode == 30 || mode == 31 || mode == 32 || mode == 34;
+         mode == 24 || mode == 25 || mode == 26 || mode == 28 || mode == 30 || mode == 31 || mode == 32;
 }
 // phase stamps of kernel mode 21 (g_stamps: STAMP_UNITS x STAMP_N)
 extern "C" int ewh_dev_stamps(long long* out, long long n) {

@@ -1012,89 +1012,15 @@ void dchol_rowpanel_kernel(double* __restrict__ mats, int Np, int k, int p0, con
 // is added (the loads pinned in place by empty asm statements).  C5 at
 // B = 512: 80.7 vs 83.6 ms (!PIPE, the slab loaded at the top of its step:
 // dev kernel mode 32), bit-identical.
-// The diagonal tile (i, i) of a later block row takes its updates of rows
-// p < p1 (the dchol_rowupdate2_kernel arithmetic in the same order: U_pi
-// column slabs in the registers of waves 0-3, the U_pi tile staged through
-// LDS by all 8 waves); dchol_rowupdate2_kernel then adds p1 <= p < i only.
-__device__ __forceinline__ void diag_tile_pre(double* __restrict__ mats, int Np, int i, int p1,
-                                              double (*Ut)[DCB + 1]) {
-  const int t = threadIdx.x, w = t >> 6, lane = t & 63, q = lane >> 4, c = lane & 15, bl = blockIdx.y;
-  const bool mma = w < 4;
-  char* cb = (char*)(mats + (long long)bl * Np * Np);
-  auto at = [&](unsigned off) -> double& { return *(double*)(cb + off); };
-  const unsigned rowb = 8u * (unsigned)Np;
-  const unsigned toff = (unsigned)(DCB * i + 16 * (w & 3) + q) * rowb + 8u * (unsigned)(DCB * i + c);
-  v4d acc[4];
-  if (mma) {
-#pragma unroll
-    for (int jb = 0; jb < 4; ++jb)
-#pragma unroll
-      for (int r = 0; r < 4; ++r) acc[jb][r] = at(toff + (unsigned)(4 * r) * rowb + 8u * (unsigned)(16 * jb));
-  }
-  const unsigned aoff = (unsigned)q * rowb + 8u * (unsigned)(DCB * i + 16 * (w & 3) + c);
-  const unsigned soff = (unsigned)(t >> 6) * rowb + 8u * (unsigned)(DCB * i + (t & 63));   // rows (t >> 6) + 8 r
-  double pb[8], a[16];
-  auto sload = [&](int p) {
-    unsigned o = soff + (unsigned)(DCB * p) * rowb;
-    asm volatile("" : "+v"(o));
-#pragma unroll
-    for (int r = 0; r < 8; ++r) pb[r] = at(o + (unsigned)(8 * r) * rowb);
-  };
-  auto ahalf = [&](int p, int h) {
-    unsigned o = aoff + (unsigned)(DCB * p) * rowb;
-    asm volatile("" : "+v"(o));
-#pragma unroll
-    for (int ts = 8 * h; ts < 8 * h + 8; ++ts) a[ts] = at(o + (unsigned)(4 * ts) * rowb);
-  };
-  sload(0);
-  if (mma) {
-    ahalf(0, 0);
-    ahalf(0, 1);
-  }
-  for (int p = 0; p < p1; ++p) {
-    const int pn = min(p + 1, p1 - 1);
-    __syncthreads();
-#pragma unroll
-    for (int r = 0; r < 8; ++r) Ut[(t >> 6) + 8 * r][t & 63] = pb[r];
-    __syncthreads();
-    sload(pn);
-    if (mma) {
-      static_for<0, 2>([&](auto H) {
-        constexpr int h = decltype(H)::value;
-#pragma unroll
-        for (int ts = 8 * h; ts < 8 * h + 8; ++ts) {
-#pragma unroll
-          for (int jb = 0; jb < 4; ++jb)
-            acc[jb] = __builtin_amdgcn_mfma_f64_16x16x4f64(a[ts], Ut[4 * ts + q][16 * jb + c], acc[jb], 0, 0, 1);
-        }
-        asm volatile("" ::: "memory");
-        ahalf(pn, h);
-        asm volatile("" ::: "memory");
-      });
-    }
-  }
-  if (mma) {
-    unsigned toff2 = toff;
-    asm volatile("" : "+v"(toff2));
-#pragma unroll
-    for (int jb = 0; jb < 4; ++jb)
-#pragma unroll
-      for (int r = 0; r < 4; ++r) at(toff2 + (unsigned)(4 * r) * rowb + 8u * (unsigned)(16 * jb)) = acc[jb][r];
-  }
-}
-
-// pre >= 0: one workgroup more per sample (blockIdx.x == the tile count)
-// runs diag_tile_pre on tile (pre, pre) = (k + 2, k + 2) over p < k, beside
-// the pair's tiles, so the next pair's diagonal-tile row update (a serial
-// chain of k steps on one workgroup per sample) takes only p = k, k + 1.
+// (Measured and dropped: one more workgroup per sample pre-updating the next
+// pair's diagonal tile over p < k, which cut the diagonal-tile row update
+// from 69 to 17 us per launch but lengthened the pair launches by more --
+// m + 1 instead of m workgroups per sample, and late pairs have m ~ 1-3:
+// 81.3 vs 79.7 ms per C5 batch.)
 template <bool PIPE>
 __global__ __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(4, 4)))
-void dchol_rowpair_kernel(double* __restrict__ mats, int Np, int k, const double* __restrict__ wbuf, int pre) {
+void dchol_rowpair_kernel(double* __restrict__ mats, int Np, int k, const double* __restrict__ wbuf) {
   __shared__ double Uk[2][DCB][DCB + 1];
-  if (pre >= 0 && (int)blockIdx.x == (int)gridDim.x - 1) {
-    diag_tile_pre(mats, Np, pre, k, Uk[0]);
-    return;
-  }
   const int t = threadIdx.x, wave = t >> 6, rt = wave >> 2, w = wave & 3;
   const int j = k + 1 + blockIdx.x, bl = blockIdx.y;
   const int lane = t & 63, q = lane >> 4, c = lane & 15;
@@ -2139,7 +2065,6 @@ int corr_finish(DevCtx* h, const double* theta_dev, int B, const double* keep, d
     // (i, j) takes the same K = 64 slabs in the same order into the same
     // accumulator (stored and reloaded in full between panels): bit-identical.
     const bool right = h->kernel_mode == 0 && nb <= CORR_RIGHT_LOOKING_MAX;
-    int pre_done = -1;                 // the diagonal tile a pair kernel pre-updated (over p < its k - 2)
     for (int k = 0; k < nbk; ++k) {
       const int m = nbk - k - 1;
       if (right) {
@@ -2166,15 +2091,11 @@ int corr_finish(DevCtx* h, const double* theta_dev, int B, const double* keep, d
       int p0 = 0;                                       // the first row p this block row still needs
       if (pairs && (k & 1)) p0 = k - 1;
       const bool pair_here = pairs && !(k & 1) && m > 0 && k > 0;
-      // the pair kernel at k also updates the diagonal tile (k + 2, k + 2) over
-      // p < k (dev mode 34: not); its row update then starts at p = k - 2 here
-      const int pre = (pair_here && k + 2 < nbk && h->kernel_mode != 34) ? k + 2 : -1;
-      const int p0_diag = (pairs && !(k & 1) && k >= 4 && pre_done == k) ? k - 2 : p0;
       if (h->kernel_mode == 1 && k > 0)     // round-1 row update (both operands staged through LDS)
         hipLaunchKernelGGL(dchol_rowupdate_kernel, dim3(m + 1, nb), dim3(256), 0, st, h->d_dense, h->Np, k);
       else if (k > 0 && h->kernel_mode != 7)   // the diagonal tile's row update only (fused), or the whole row
         hipLaunchKernelGGL(dchol_rowupdate2_kernel, dim3(fused ? 1 : m + 1, nb), dim3(256), 0, st, h->d_dense, h->Np,
-                           k, fused ? p0_diag : p0);
+                           k, p0);
 
       if (h->kernel_mode == 7 || h->kernel_mode == 1) {   // A/B: round-1 LDS diagonal block + LDS-staged panel
         hipLaunchKernelGGL(dchol_diag_kernel, dim3(nb), dim3(256), 0, st, h->d_dense, h->Np, k, h->d_wbuf,
@@ -2194,15 +2115,14 @@ int corr_finish(DevCtx* h, const double* theta_dev, int B, const double* keep, d
             hipLaunchKernelGGL(HIP_KERNEL_NAME(dchol_rowpanel_kernel<1>), dim3(m, nb), dim3(256), 0, st, h->d_dense,
                                h->Np, k, 0, h->d_wbuf);
           else if (pair_here && h->kernel_mode == 32)   // (dev A/B: U_pj loaded at the top of each step)
-            hipLaunchKernelGGL(HIP_KERNEL_NAME(dchol_rowpair_kernel<false>), dim3(m + (pre >= 0), nb), dim3(512), 0,
-                               st, h->d_dense, h->Np, k, h->d_wbuf, pre);
+            hipLaunchKernelGGL(HIP_KERNEL_NAME(dchol_rowpair_kernel<false>), dim3(m, nb), dim3(512), 0, st,
+                               h->d_dense, h->Np, k, h->d_wbuf);
           else if (pair_here)         // rows k and k + 1 over p < k, row k's panel
-            hipLaunchKernelGGL(HIP_KERNEL_NAME(dchol_rowpair_kernel<true>), dim3(m + (pre >= 0), nb), dim3(512), 0,
-                               st, h->d_dense, h->Np, k, h->d_wbuf, pre);
+            hipLaunchKernelGGL(HIP_KERNEL_NAME(dchol_rowpair_kernel<true>), dim3(m, nb), dim3(512), 0, st,
+                               h->d_dense, h->Np, k, h->d_wbuf);
           else
             hipLaunchKernelGGL(HIP_KERNEL_NAME(dchol_rowpanel_kernel<2>), dim3((m + 1) / 2, nb), dim3(512), 0, st,
                                h->d_dense, h->Np, k, p0, h->d_wbuf);
-          if (pair_here && h->kernel_mode != 28) pre_done = pre;
         }
         else if (m > 0)
           hipLaunchKernelGGL(dchol_panel_reg_kernel, dim3(4 * m, nb), dim3(64), 0, st, h->d_dense, h->Np, k,
@@ -3181,7 +3101,7 @@ int ewh_set_fixed_white(ewh_handle* H, const double* values) {
 }
 
 int ewh_set_kernel_mode(ewh_handle* H, int32_t mode) {
-  if (!H || mode < 0 || mode > 34) return set_err(EWH_E_INVALID, "bad handle / mode");
+  if (!H || mode < 0 || mode > 32) return set_err(EWH_E_INVALID, "bad handle / mode");
   if (mode != 0 && mode != 1 && mode != 2 && mode != 7 && mode != MODE_WIDE && mode != MODE_DD && !variant_built(mode))
     return set_err(EWH_E_UNSUPPORTED, "kernel mode " + std::to_string(mode) +
                                           " is not built into this library (A/B variants: the dev library, make dev)");
