@@ -289,8 +289,12 @@ int ewh_transfer_stats(const ewh_handle* h, int64_t* h2d_bytes, int64_t* peer);
  * stamps (ewh_dev_lat_stamps), 23 = the latency kernel with every wait
  * forced to run out (the stall error path), 24 / 25 = the latency kernel with
  * block barriers instead of the dataflow panel loop / as in round 3, 26 = the
- * C3 kernel at one wave per SIMD with the whole triangle resident.  Other
- * modes return EWH_E_UNSUPPORTED. */
+ * C3 kernel at one wave per SIMD with the whole triangle resident, 28 = the
+ * C5 row update one 64-row block row per pass with one tile per workgroup
+ * (round 3), 30 = the contraction with TwoSum accumulation (up to 10
+ * blocks), 31 = the C5 row update one block row per pass with two tiles per
+ * workgroup, 32 = the C5 two-row pass with each streamed slab loaded at the
+ * top of its step.  Other modes return EWH_E_UNSUPPORTED. */
 int ewh_set_kernel_mode(ewh_handle* h, int32_t mode);
 
 void ewh_destroy(ewh_handle* h);
