@@ -1395,6 +1395,10 @@ struct DevCtx {
   // latency path of small single-device batches (chol_lat.hip): every pulsar
   // has the same reduced block count lat_nb <= LAT_NB_MAX (0: not eligible)
   int lat_nb = 0;
+  // correlated process: a second stream on which the M_g inverses of the
+  // first sample chunk run beside the per-pulsar partial factorisations
+  hipStream_t side = nullptr;
+  hipEvent_t ev_fork = nullptr, ev_join = nullptr;
   // multi-context batches: the theta entries this context's units read,
   // packed in pinned host memory (h_stage), copied to d_stage and scattered
   // into d_theta by expand_theta_kernel along the segment table d_seg
@@ -2039,20 +2043,29 @@ int corr_partial(DevCtx* h, const double* theta_dev, int B, int p_begin, int p_e
 // Step 2, once every pulsar's kept block is in `keep`: per sample chunk the
 // M_g inverses, the dense Sigma_c assembly and factorisation; the global term
 // of sample b goes to units[P B + b].
-int corr_finish(DevCtx* h, const double* theta_dev, int B, const double* keep, double* units, hipStream_t st) {
-  const int P = h->P, ldth = h->n_param, KD = 16 * h->keep;
+// the M_g inverses and log-determinants of samples [c0, c0 + nb)
+void launch_minv(DevCtx* h, const double* theta_dev, int c0, int nb, hipStream_t st) {
+  const int P = h->P, ldth = h->n_param;
+  const size_t lds = ((size_t)P * (P + 1) + 3 * P) * sizeof(double);
+  if (P <= MINV_PMAX && h->kernel_mode != 7)
+    hipLaunchKernelGGL(common_minv_reg_kernel, dim3(h->nuniq, nb), dim3(512), 0, st, h->d_cps, P, h->d_orf,
+                       h->d_cspec, h->nc, h->d_cuniq, theta_dev, ldth, c0, h->d_minv, h->d_mlog);
+  else
+    hipLaunchKernelGGL(common_minv_kernel, dim3(h->nuniq, nb), dim3(256), lds, st, h->d_cps, P, h->d_orf,
+                       h->d_cspec, h->nc, h->d_cuniq, theta_dev, ldth, c0, h->d_minv, h->d_mlog);
+}
+
+// first_minv_done: the M_g inverses of the first chunk are already in
+// d_minv (lnl_correlated ran them beside the partial factorisations)
+int corr_finish(DevCtx* h, const double* theta_dev, int B, const double* keep, double* units, hipStream_t st,
+                bool first_minv_done = false) {
+  const int P = h->P, KD = 16 * h->keep;
   int rc;
   if ((rc = ensure_common_scratch(h, B))) return rc;
   const int nbk = h->Np / DCB;
-  const size_t lds = ((size_t)P * (P + 1) + 3 * P) * sizeof(double);
   for (int c0 = 0; c0 < B; c0 += h->cchunk) {
     const int nb = std::min(h->cchunk, B - c0);
-    if (P <= MINV_PMAX && h->kernel_mode != 7)
-      hipLaunchKernelGGL(common_minv_reg_kernel, dim3(h->nuniq, nb), dim3(512), 0, st, h->d_cps, P, h->d_orf,
-                         h->d_cspec, h->nc, h->d_cuniq, theta_dev, ldth, c0, h->d_minv, h->d_mlog);
-    else
-      hipLaunchKernelGGL(common_minv_kernel, dim3(h->nuniq, nb), dim3(256), lds, st, h->d_cps, P, h->d_orf,
-                         h->d_cspec, h->nc, h->d_cuniq, theta_dev, ldth, c0, h->d_minv, h->d_mlog);
+    if (!(first_minv_done && c0 == 0)) launch_minv(h, theta_dev, c0, nb, st);
     hipLaunchKernelGGL(common_assemble_kernel, dim3((h->Np + 3) / 4, nb), dim3(256), 0, st, keep, KD, P, h->nc,
                        (long long)B, c0, h->d_minv, h->d_crep, h->Np, h->d_dense);
     EWH_HIP(hipMemsetAsync(h->d_cldet, 0, sizeof(double) * nb, st));
@@ -2141,9 +2154,25 @@ int corr_finish(DevCtx* h, const double* theta_dev, int B, const double* keep, d
 // correlated batch on one device: step 1 for every pulsar, then step 2
 int lnl_correlated(DevCtx* h, const double* theta_dev, int B, hipStream_t st) {
   int rc;
-  if ((rc = ensure_keep(h, B)) || (rc = corr_partial(h, theta_dev, B, 0, h->P, h->d_units, h->d_keep, st)))
-    return rc;
-  return corr_finish(h, theta_dev, B, h->d_keep, h->d_units, st);
+  if ((rc = ensure_keep(h, B)) || (rc = ensure_common_scratch(h, B))) return rc;
+  // the first chunk's M_g inverses depend on theta only: they run on the
+  // side stream while the partial factorisations run on st (forked after
+  // whatever st produced theta with; joined before the assembly)
+  const bool overlap = h->P <= MINV_PMAX && h->kernel_mode != 7;
+  if (overlap) {
+    if (!h->side) {
+      EWH_HIP(hipStreamCreateWithFlags(&h->side, hipStreamNonBlocking));
+      EWH_HIP(hipEventCreateWithFlags(&h->ev_fork, hipEventDisableTiming));
+      EWH_HIP(hipEventCreateWithFlags(&h->ev_join, hipEventDisableTiming));
+    }
+    EWH_HIP(hipEventRecord(h->ev_fork, st));
+    EWH_HIP(hipStreamWaitEvent(h->side, h->ev_fork, 0));
+    launch_minv(h, theta_dev, 0, std::min(h->cchunk, B), h->side);
+    EWH_HIP(hipEventRecord(h->ev_join, h->side));
+  }
+  if ((rc = corr_partial(h, theta_dev, B, 0, h->P, h->d_units, h->d_keep, st))) return rc;
+  if (overlap) EWH_HIP(hipStreamWaitEvent(st, h->ev_join, 0));
+  return corr_finish(h, theta_dev, B, h->d_keep, h->d_units, st, overlap);
 }
 
 }  // namespace
@@ -2157,7 +2186,11 @@ void destroy_ctx(DevCtx* h) {
   drop_graphs(h);
   if (h->h_stage) (void)hipHostFree(h->h_stage);
   if (h->h_seg) (void)hipHostFree(h->h_seg);
+  if (h->side) (void)hipStreamSynchronize(h->side);
   for (void* p : h->allocs) (void)hipFree(p);
+  if (h->ev_fork) (void)hipEventDestroy(h->ev_fork);
+  if (h->ev_join) (void)hipEventDestroy(h->ev_join);
+  if (h->side) (void)hipStreamDestroy(h->side);
   if (h->stream) (void)hipStreamDestroy(h->stream);
   delete h;
 }
