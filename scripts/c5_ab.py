@@ -19,11 +19,13 @@ def main():
     ap.add_argument("--modes", default="0,28")
     ap.add_argument("--rounds", type=int, default=5)
     ap.add_argument("--B", type=int, default=512)
+    ap.add_argument("--n-psr", type=int, default=100)
+    ap.add_argument("--n-toa", type=int, default=20000)
     args = ap.parse_args()
     import torch
     from bench import FP64_MFMA_PEAK_TFLOPS
     from enterprise_warp_amd import synth
-    cfg = synth.config_c5()
+    cfg = synth.config_c5(n_psr=args.n_psr, n_toa=args.n_toa)
     pta = cfg.pta
     eng = pta.engine(0)
     P, B = len(pta.signal_collections), args.B
@@ -57,7 +59,8 @@ def main():
                             "fp64_mfma_frac": flops / (ms * 1e-3) / 1e12 / FP64_MFMA_PEAK_TFLOPS,
                             "bit_identical_to_first": bool(np.array_equal(vals[md], vals[modes[0]]))}
     print(json.dumps(res, indent=1))
+    return 0 if all(r["bit_identical_to_first"] for r in res.values()) else 1
 
 
 if __name__ == "__main__":
-    main()
+    sys.exit(main())

@@ -50,3 +50,20 @@ def test_latency_stall_is_an_error():
                        capture_output=True, text=True, timeout=600, env=env)
     print(r.stdout[-4000:], r.stderr[-2000:])
     assert r.returncode == 0
+
+
+def test_c5_row_update_variants_bit_identical():
+    """The C5 row-update schedules of the dev library (28: one block row per
+    pass, one tile per workgroup -- round 3; 31: one row per pass, two tiles;
+    32: the two-row pass with each streamed slab loaded at the top of its
+    step) against the default (two rows per pass, pipelined slabs): the same
+    lnL bit for bit (scripts/c5_ab.py on a 20-pulsar HD model, 9 block rows)."""
+    lib = os.path.join(ROOT, "enterprise_warp_amd", "libewarp_hip_dev.so")
+    if not os.path.exists(lib):
+        pytest.skip("dev library not built (make -C enterprise_warp_amd/csrc dev)")
+    env = dict(os.environ, EWARP_HIP_LIB=lib)
+    r = subprocess.run([sys.executable, os.path.join(ROOT, "scripts", "c5_ab.py"), "--modes", "0,28,31,32",
+                        "--rounds", "1", "--n-psr", "20", "--n-toa", "1200", "--B", "64"],
+                       capture_output=True, text=True, timeout=600, env=env)
+    print(r.stdout[-4000:], r.stderr[-2000:])
+    assert r.returncode == 0
