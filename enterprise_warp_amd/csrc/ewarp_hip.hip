@@ -1955,6 +1955,11 @@ int setup_common(DevCtx* h, const ewh_pta_desc* d) {
   for (int p = 0; p < P; ++p) cps[p] = common_psr(p);
   if ((rc = dupload(h, &h->d_cps, cps.data(), cps.size()))) return rc;
   h->Np = DCB * ((P * h->nc + 1 + DCB - 1) / DCB);
+  // the dense kernels address a sample's Sigma_c by 32-bit byte offsets
+  // (dchol_rowpair_kernel, dchol_rowupdate2_kernel): < 4 GB per sample
+  if ((double)h->Np * h->Np * 8.0 >= 4294967296.0)
+    return set_err(EWH_E_UNSUPPORTED, "correlated common process: Sigma_c of " + std::to_string(h->Np) +
+                                          " columns exceeds 4 GB per sample (P x common columns <= 23168)");
   const double per = (double)h->Np * h->Np * 8.0;
   h->cchunk_cap = (int)std::max(1.0, std::min(1024.0, 40.0e9 / per));   // <= 40 GB of dense Sigma_c per chunk
   h->cchunk = 0;              // the chunk scratch is allocated on first use, sized to the batch
