@@ -2911,7 +2911,10 @@ int lnl_batch_corr_pulsars(ewh_handle* H, int B, double* out_host) {
 // otherwise run the batch eagerly (that also sizes every scratch buffer) and
 // capture the same sequence for the next call.
 constexpr uint64_t LAT_SENTINEL = 0x7ff4dead0ebeef01ull;   // a NaN no kernel writes
-constexpr int LAT_B_MAX = 8;    // batches up to this size take the latency kernel (profiles/r03c/latency.log: B = 16 is faster batched)
+// batches up to this size take the latency kernel (round 4, interleaved on
+// C3: B = 12 / 16 / 24 at 57.9 / 57.5 / 80.0 us vs 64.2 / 65.8 / 83.3 us
+// batched; B = 32 even, larger batched -- profiles/r04d/latency_sweep_bmax.log)
+constexpr int LAT_B_MAX = 24;
 
 int lnl_batch_single(ewh_handle* H, DevCtx* h, int B, double* out_host) {
   int rc;

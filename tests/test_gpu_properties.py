@@ -154,23 +154,27 @@ def test_set_fixed_white_in_place(require_gpu):
 
 def test_graph_replay_matches_eager(require_gpu):
     """ewh_lnl_batch captures each single-device batch size above the latency
-    path's (B > 8) into a HIP graph on its first call and replays it
-    afterwards; buffer growth (a larger B) invalidates the graphs.  Every call
-    must equal the first (eager) one; single-theta calls (the latency kernel)
-    are deterministic and agree with the batched value."""
+    path's (B > LAT_B_MAX = 24) into a HIP graph on its first call and
+    replays it afterwards; buffer growth (a larger B) invalidates the graphs.
+    Every call must equal the first (eager) one; single-theta calls (the
+    latency kernel) are deterministic, agree with a 16-sample latency batch
+    bit for bit and with the batched value."""
     from conftest import load_golden
     pta, X, _, _ = load_golden("c3_small")
+    X32 = np.vstack([X, X])
     big = np.vstack([X] * 32)
-    ref = {1: pta.get_lnlikelihood_batch(X[:1]), 16: pta.get_lnlikelihood_batch(X)}
+    ref = {1: pta.get_lnlikelihood_batch(X[:1]), 16: pta.get_lnlikelihood_batch(X),
+           32: pta.get_lnlikelihood_batch(X32)}
     ref[512] = pta.get_lnlikelihood_batch(big)
-    for B in (1, 1, 16, 1, 16, 512, 1, 16, 512, 1):
-        XX = {1: X[:1], 16: X, 512: big}[B]
+    for B in (1, 1, 32, 16, 1, 32, 512, 1, 32, 16, 512, 1):
+        XX = {1: X[:1], 16: X, 32: X32, 512: big}[B]
         np.testing.assert_array_equal(pta.get_lnlikelihood_batch(XX), ref[B])
     for i in range(16):                                   # single-theta calls (PTMCMC / bilby)
         one = pta.get_lnlikelihood(X[i])                  # (the latency kernel: B = 1 <= LAT_B_MAX)
         assert one == pta.get_lnlikelihood_batch(X[i:i + 1])[0]
+        assert one == ref[16][i]                          # (B = 16: the latency kernel too)
         # ... the batched kernels' value up to the re-associated log-determinant sum
-        assert abs(one - ref[16][i]) <= 1e-3 * (1e-6 + 1e-10 * abs(ref[16][i]))
+        assert abs(one - ref[32][i]) <= 1e-3 * (1e-6 + 1e-10 * abs(ref[32][i]))
 
 
 def test_correlated_pulsar_partition(require_gpu):
