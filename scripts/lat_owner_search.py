@@ -18,6 +18,7 @@ import math
 import random
 
 M, F, OV = 130.0, 2500.0, 600.0
+UNEXT = 0.0     # --unext: cycles per panel when U (bb, bb+1) is formed by another wave than the lookahead owner
 
 
 def cost(nb, own):
@@ -33,6 +34,8 @@ def cost(nb, own):
                     tr[own[(i, j)]] += 4
         o = own[(bb + 1, bb + 1)]
         tot += M * max(rv) + max(tr[w] * M + ((4 * M + F) if w == o else 0.0) for w in range(4)) + OV
+        if own[(bb, bb + 1)] != o:
+            tot += UNEXT
     return tot
 
 
@@ -60,8 +63,20 @@ def search(nb, seed=1, restarts=24, iters=20000):
 
 
 def main():
+    import argparse
+    global UNEXT
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--unext", type=float, default=0.0,
+                    help="penalty (cycles) per panel whose U (bb, bb+1) another wave than the lookahead owner forms "
+                         "(its LDS publish / wait; round 4 A/B)")
+    ap.add_argument("--nb", type=int, default=0, help="only this NB")
+    args = ap.parse_args()
+    UNEXT = args.unext
     rows = []
     for nb in range(1, 9):
+        if args.nb and nb != args.nb:
+            rows.append([[0] * 8 for _ in range(8)])
+            continue
         base = {(i, j): (i + j) & 3 for i in range(nb) for j in range(i, nb)}
         if nb == 1:
             c, own = cost(nb, base), base
