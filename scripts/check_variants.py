@@ -20,7 +20,7 @@ import numpy as np  # noqa: E402
 
 def main():
     ap = argparse.ArgumentParser()
-    ap.add_argument("--modes", default="0,2,17,19,21,22,23,24,25,26")
+    ap.add_argument("--modes", default="0,2,17,19,21,22,24,25,26")
     args = ap.parse_args()
     from conftest import check_parity, oracle_lnl
     from enterprise_warp_amd import synth
