@@ -405,7 +405,7 @@ class Engine:
             ("ewh_lnl_batch", self.lib))
         self._small_args = (self.h, self._small.ctypes.data, self._small_out.ctypes.data)
 
-    SMALL_B = 8
+    SMALL_B = 24     # (the latency kernel's batch bound, LAT_B_MAX in csrc/ewarp_hip.hip)
 
     def lnl_batch(self, theta):
         theta = np.ascontiguousarray(theta, dtype=float)
