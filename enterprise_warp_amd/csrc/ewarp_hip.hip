@@ -708,9 +708,26 @@ __global__ __launch_bounds__(64) void dchol_panel_reg_kernel(double* __restrict_
   });
 }
 
-// stage a 64 x 64 tile (row stride ld) into LDS [64][64 + 1]
+// stage a 64 x 64 tile (row stride ld, 16-byte aligned rows) into LDS
+// [64][64 + 1] with 256 threads: all eight 16-byte loads of a thread issued
+// before its first LDS write (a rolled loop waited on each load in turn --
+// 16 dependent global round trips per tile, most of the right-looking update
+// kernel's time at B = 1)
+typedef double v2d __attribute__((ext_vector_type(2)));
 __device__ __forceinline__ void stage64(double (*dst)[DCB + 1], const double* src, long long ld) {
-  for (int idx = threadIdx.x; idx < DCB * DCB; idx += 256) dst[idx / DCB][idx % DCB] = src[(long long)(idx / DCB) * ld + idx % DCB];
+  constexpr int NIT = DCB * DCB / 2 / 256;
+  v2d v[NIT];
+#pragma unroll
+  for (int it = 0; it < NIT; ++it) {
+    const int p = threadIdx.x + 256 * it;
+    v[it] = *(const v2d*)(src + (long long)(p >> 5) * ld + 2 * (p & 31));
+  }
+#pragma unroll
+  for (int it = 0; it < NIT; ++it) {
+    const int p = threadIdx.x + 256 * it;
+    dst[p >> 5][2 * (p & 31)] = v[it][0];
+    dst[p >> 5][2 * (p & 31) + 1] = v[it][1];
+  }
 }
 
 // Panel: U_kj = W A_kj for the blocks j > k of every sample (in place).
