@@ -607,11 +607,12 @@ struct DiagHook : NoHook {
 // residual column except in the LAST block, whose last pivot is
 // q_c = rho - d'^T Sigma_c^-1 d'); log-det and positivity accumulated; E_s,
 // D_s^-1/2 and U_st written for dchol_panel_reg_kernel.
+// (body shared with dchol_update_diag_kernel: one wave, sample bl)
 template <bool LAST>
-__global__ __launch_bounds__(64) void dchol_diag_reg_kernel(double* __restrict__ mats, int Np, int k,
-                                                            double* __restrict__ wbuf, double* __restrict__ ldet,
-                                                            double* __restrict__ qout, int* __restrict__ fail) {
-  const int bl = blockIdx.x, lane = threadIdx.x, q = lane >> 4, c = lane & 15;
+__device__ __forceinline__ void diag_reg_body(double* __restrict__ mats, int Np, int k, double* __restrict__ wbuf,
+                                              double* __restrict__ ldet, double* __restrict__ qout,
+                                              int* __restrict__ fail, int bl, int lane) {
+  const int q = lane >> 4, c = lane & 15;
   const double* A = mats + (long long)bl * Np * Np + (long long)(DCB * k) * Np + DCB * k;
   double* W = wbuf + (long long)bl * DW_SLOTS * 256 + lane * 4;
   constexpr auto id = [](int i, int j) { return i * 4 - i * (i - 1) / 2 + (j - i); };
@@ -661,6 +662,13 @@ __global__ __launch_bounds__(64) void dchol_diag_reg_kernel(double* __restrict__
     if (!ok_all) fail[bl] = 1;
     if (LAST) qout[bl] = qv;
   }
+}
+
+template <bool LAST>
+__global__ __launch_bounds__(64) void dchol_diag_reg_kernel(double* __restrict__ mats, int Np, int k,
+                                                            double* __restrict__ wbuf, double* __restrict__ ldet,
+                                                            double* __restrict__ qout, int* __restrict__ fail) {
+  diag_reg_body<LAST>(mats, Np, k, wbuf, ldet, qout, fail, blockIdx.x, threadIdx.x);
 }
 
 // U_kj = L_kk^-1 A_kj (scaled) for the tiles j > k: one wave per (16-column
@@ -757,7 +765,7 @@ __global__ __launch_bounds__(256) void dchol_panel_kernel(double* __restrict__ m
 
 // Trailing update A_ij -= U_ki^T U_kj, k < i <= j, every sample.
 // grid (T(k), Bc) with T(k) = m (m + 1) / 2, m = nb - k - 1.
-__global__ __launch_bounds__(256) void dchol_update_kernel(double* __restrict__ mats, int Np, int k) {
+__device__ __forceinline__ void update_tile_body(double* __restrict__ mats, int Np, int k) {
   __shared__ double Ui[DCB][DCB + 1];
   __shared__ double Uj[DCB][DCB + 1];
   const int nb = Np / DCB, m = nb - k - 1;
@@ -786,6 +794,27 @@ __global__ __launch_bounds__(256) void dchol_update_kernel(double* __restrict__ 
   for (int jb = 0; jb < 4; ++jb)
 #pragma unroll
     for (int r = 0; r < 4; ++r) Aij[(long long)(16 * w + q + 4 * r) * Np + 16 * jb + c] = acc[jb][r];
+}
+
+__global__ __launch_bounds__(256) void dchol_update_kernel(double* __restrict__ mats, int Np, int k) {
+  update_tile_body(mats, Np, k);
+}
+
+// The trailing update of step k with the diagonal block k + 1 factored in
+// the same launch: workgroup 0 of each sample owns tile (k + 1, k + 1);
+// after storing it, its first wave runs the diagonal factorisation of
+// dchol_diag_reg_kernel on it (same values, same code: bit-identical) while
+// the other workgroups are still updating their tiles -- one launch and one
+// dependent gap fewer per block row of the one-proposal schedule.  Nothing
+// else reads the block-(k + 1) operands in wbuf before the next panel.
+template <bool LAST>
+__global__ __launch_bounds__(256) void dchol_update_diag_kernel(double* __restrict__ mats, int Np, int k,
+                                                                double* __restrict__ wbuf, double* __restrict__ ldet,
+                                                                double* __restrict__ qout, int* __restrict__ fail) {
+  update_tile_body(mats, Np, k);
+  if (blockIdx.x != 0) return;
+  __syncthreads();   // the tile's rows stored by every wave of the workgroup
+  if (threadIdx.x < 64) diag_reg_body<LAST>(mats, Np, k + 1, wbuf, ldet, qout, fail, blockIdx.y, threadIdx.x);
 }
 
 // Row-oriented (left-looking) update, the default: before block row i is
@@ -2099,19 +2128,31 @@ int corr_finish(DevCtx* h, const double* theta_dev, int B, const double* keep, d
     // K = 64 k accumulation of one tile is a serial chain on one CU.  Tile
     // (i, j) takes the same K = 64 slabs in the same order into the same
     // accumulator (stored and reloaded in full between panels): bit-identical.
-    const bool right = h->kernel_mode == 0 && nb <= CORR_RIGHT_LOOKING_MAX;
+    const bool right = (h->kernel_mode == 0 || h->kernel_mode == 33) && nb <= CORR_RIGHT_LOOKING_MAX;
     for (int k = 0; k < nbk; ++k) {
       const int m = nbk - k - 1;
       if (right) {
-        if (m == 0) {
-          hipLaunchKernelGGL(HIP_KERNEL_NAME(dchol_diag_reg_kernel<true>), dim3(nb), dim3(64), 0, st, h->d_dense,
-                             h->Np, k, h->d_wbuf, h->d_cldet, h->d_cq, h->d_cfail);
-          continue;
+        // the diagonal block k + 1 is factored inside the update launch of
+        // step k (dchol_update_diag_kernel); dev mode 33 launches it apart
+        const bool fuse_diag = h->kernel_mode != 33;
+        if (k == 0 || !fuse_diag) {
+          if (m == 0)
+            hipLaunchKernelGGL(HIP_KERNEL_NAME(dchol_diag_reg_kernel<true>), dim3(nb), dim3(64), 0, st, h->d_dense,
+                               h->Np, k, h->d_wbuf, h->d_cldet, h->d_cq, h->d_cfail);
+          else
+            hipLaunchKernelGGL(HIP_KERNEL_NAME(dchol_diag_reg_kernel<false>), dim3(nb), dim3(64), 0, st, h->d_dense,
+                               h->Np, k, h->d_wbuf, h->d_cldet, h->d_cq, h->d_cfail);
         }
-        hipLaunchKernelGGL(HIP_KERNEL_NAME(dchol_diag_reg_kernel<false>), dim3(nb), dim3(64), 0, st, h->d_dense,
-                           h->Np, k, h->d_wbuf, h->d_cldet, h->d_cq, h->d_cfail);
+        if (m == 0) continue;
         hipLaunchKernelGGL(dchol_panel_reg_kernel, dim3(4 * m, nb), dim3(64), 0, st, h->d_dense, h->Np, k, h->d_wbuf);
-        hipLaunchKernelGGL(dchol_update_kernel, dim3(m * (m + 1) / 2, nb), dim3(256), 0, st, h->d_dense, h->Np, k);
+        if (!fuse_diag)
+          hipLaunchKernelGGL(dchol_update_kernel, dim3(m * (m + 1) / 2, nb), dim3(256), 0, st, h->d_dense, h->Np, k);
+        else if (m == 1)   // block k + 1 is the last one (its pivot q_c)
+          hipLaunchKernelGGL(HIP_KERNEL_NAME(dchol_update_diag_kernel<true>), dim3(1, nb), dim3(256), 0, st,
+                             h->d_dense, h->Np, k, h->d_wbuf, h->d_cldet, h->d_cq, h->d_cfail);
+        else
+          hipLaunchKernelGGL(HIP_KERNEL_NAME(dchol_update_diag_kernel<false>), dim3(m * (m + 1) / 2, nb), dim3(256),
+                             0, st, h->d_dense, h->Np, k, h->d_wbuf, h->d_cldet, h->d_cq, h->d_cfail);
         continue;
       }
       // default for large sample chunks: row update + panel fused (the updated
@@ -3161,8 +3202,14 @@ int ewh_set_fixed_white(ewh_handle* H, const double* values) {
 }
 
 int ewh_set_kernel_mode(ewh_handle* H, int32_t mode) {
-  if (!H || mode < 0 || mode > 32) return set_err(EWH_E_INVALID, "bad handle / mode");
-  if (mode != 0 && mode != 1 && mode != 2 && mode != 7 && mode != MODE_WIDE && mode != MODE_DD && !variant_built(mode))
+  if (!H || mode < 0 || mode > 33) return set_err(EWH_E_INVALID, "bad handle / mode");
+#ifdef EWH_DEV
+  constexpr bool dev_lib = true;   // mode 33 (the one-proposal C5 schedule with the diagonal launched apart)
+#else
+  constexpr bool dev_lib = false;
+#endif
+  if (mode != 0 && mode != 1 && mode != 2 && mode != 7 && mode != MODE_WIDE && mode != MODE_DD && !variant_built(mode) &&
+      !(mode == 33 && dev_lib))
     return set_err(EWH_E_UNSUPPORTED, "kernel mode " + std::to_string(mode) +
                                           " is not built into this library (A/B variants: the dev library, make dev)");
   for (DevCtx* h : H->ctx) {

@@ -294,7 +294,9 @@ int ewh_transfer_stats(const ewh_handle* h, int64_t* h2d_bytes, int64_t* peer);
  * (round 3), 30 = the contraction with TwoSum accumulation (up to 10
  * blocks), 31 = the C5 row update one block row per pass with two tiles per
  * workgroup, 32 = the C5 two-row pass with each streamed slab loaded at the
- * top of its step.  Other modes return EWH_E_UNSUPPORTED. */
+ * top of its step, 33 = the C5 one-proposal (right-looking) schedule with
+ * each diagonal block factored in a launch of its own instead of inside the
+ * previous trailing update.  Other modes return EWH_E_UNSUPPORTED. */
 int ewh_set_kernel_mode(ewh_handle* h, int32_t mode);
 
 void ewh_destroy(ewh_handle* h);
