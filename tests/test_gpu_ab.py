@@ -67,3 +67,20 @@ def test_c5_row_update_variants_bit_identical():
                        capture_output=True, text=True, timeout=600, env=env)
     print(r.stdout[-4000:], r.stderr[-2000:])
     assert r.returncode == 0
+
+
+@pytest.mark.parametrize("B", [1, 3])
+def test_c5_one_proposal_diag_fusion_bit_identical(B):
+    """The one-proposal (right-looking) C5 schedule factors diagonal block
+    k + 1 inside the step-k trailing update; dev mode 33 launches it apart:
+    the same lnL bit for bit (against the left-looking schedule:
+    test_gpu_properties.py::test_correlated_right_looking_small_chunks)."""
+    lib = os.path.join(ROOT, "enterprise_warp_amd", "libewarp_hip_dev.so")
+    if not os.path.exists(lib):
+        pytest.skip("dev library not built (make -C enterprise_warp_amd/csrc dev)")
+    env = dict(os.environ, EWARP_HIP_LIB=lib)
+    r = subprocess.run([sys.executable, os.path.join(ROOT, "scripts", "c5_ab.py"), "--modes", "0,33",
+                        "--rounds", "1", "--n-psr", "20", "--n-toa", "1200", "--B", str(B)],
+                       capture_output=True, text=True, timeout=600, env=env)
+    print(r.stdout[-4000:], r.stderr[-2000:])
+    assert r.returncode == 0
