@@ -471,9 +471,15 @@ __global__ __launch_bounds__(256) void common_assemble_kernel(const double* __re
                                                               long long Bk, int b0,
                                                               const double* __restrict__ minv,
                                                               const int* __restrict__ rep, int Np,
-                                                              double* __restrict__ mats) {
+                                                              double* __restrict__ mats, double* __restrict__ cldet,
+                                                              double* __restrict__ cq, int* __restrict__ cfail) {
   typedef double d2 __attribute__((ext_vector_type(2)));
   const int i = 4 * blockIdx.x + (threadIdx.x >> 6), lane = threadIdx.x & 63, bl = blockIdx.y;
+  if (blockIdx.x == 0 && threadIdx.x == 0) {   // the factorisation's per-sample accumulators (no memset launches)
+    cldet[bl] = 0.0;
+    cq[bl] = 0.0;
+    cfail[bl] = 0;
+  }
   if (i >= Np) return;
   const int N = P * nc;
   const float rnc = 1.0f / (float)nc;
@@ -2118,10 +2124,7 @@ int corr_finish(DevCtx* h, const double* theta_dev, int B, const double* keep, d
     const int nb = std::min(h->cchunk, B - c0);
     if (!(first_minv_done && c0 == 0)) launch_minv(h, theta_dev, c0, nb, st);
     hipLaunchKernelGGL(common_assemble_kernel, dim3((h->Np + 3) / 4, nb), dim3(256), 0, st, keep, KD, P, h->nc,
-                       (long long)B, c0, h->d_minv, h->d_crep, h->Np, h->d_dense);
-    EWH_HIP(hipMemsetAsync(h->d_cldet, 0, sizeof(double) * nb, st));
-    EWH_HIP(hipMemsetAsync(h->d_cq, 0, sizeof(double) * nb, st));
-    EWH_HIP(hipMemsetAsync(h->d_cfail, 0, sizeof(int) * nb, st));
+                       (long long)B, c0, h->d_minv, h->d_crep, h->Np, h->d_dense, h->d_cldet, h->d_cq, h->d_cfail);
     // one or a few proposals (PTMCMC): right-looking -- after each panel the
     // trailing tiles (i, j > k) are updated in parallel (m (m + 1) / 2 tiles
     // per launch, K = 64), instead of the left-looking row update whose
