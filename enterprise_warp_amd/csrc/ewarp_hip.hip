@@ -368,8 +368,10 @@ __global__ __launch_bounds__(256) void common_minv_kernel(const CommonPsr* __res
 // select and 338 registers at one wave per SIMD, took 6.7 ms per C5 batch of
 // 512; the same arithmetic in the same order: bit-identical).
 constexpr int MINV_PMAX = 128;
-// sample chunks up to this size factor Sigma_c right-looking (corr_finish)
-constexpr int CORR_RIGHT_LOOKING_MAX = 4;
+// sample chunks up to this size factor Sigma_c right-looking (corr_finish):
+// C5 right- vs left-looking per chunk, ms (profiles/r04g/xover_B*.log):
+// B = 4 1.67 / 3.21, 8 2.62 / 3.53, 12 3.65 / 4.01, 16 4.72 / 4.59
+constexpr int CORR_RIGHT_LOOKING_MAX = 12;
 
 __global__ __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(4, 4))) void common_minv_reg_kernel(const CommonPsr* __restrict__ cps, int P,
                                                               const double* __restrict__ orf,

@@ -254,8 +254,8 @@ def test_latency_kernel_matches_batched(require_gpu, c3, name):
 
 
 def test_correlated_right_looking_small_chunks(require_gpu):
-    """Sigma_c of a correlated common process: chunks of up to 4 samples (a
-    PTMCMC proposal) are factored right-looking (trailing tiles updated in
+    """Sigma_c of a correlated common process: chunks of up to 12 samples (a
+    PTMCMC proposal, a few tempering chains) are factored right-looking (trailing tiles updated in
     parallel after each 64-wide panel), larger chunks left-looking (row
     update, fused with the panel from 64 samples on).  Tile (i, j) takes the
     same K = 64 slabs in the same order either way, so the two give the same
@@ -264,7 +264,7 @@ def test_correlated_right_looking_small_chunks(require_gpu):
     pta, X, _, _ = load_golden("c5_small")
     big = np.vstack([X] * 8)                    # 128 samples: left-looking, fused row update + panel
     left = pta.get_lnlikelihood_batch(big)[:len(X)]
-    for B in (1, 3, 4):
+    for B in (1, 3, 4, 12, 13):          # 13: the left-looking small-chunk row update
         got = np.concatenate([pta.get_lnlikelihood_batch(X[i:i + B]) for i in range(0, len(X), B)])
         np.testing.assert_array_equal(got, left)
 
