@@ -10,10 +10,20 @@ equal cost (enterprise_warp_amd.sharding), each rank runs its range on its
 GPU (ewh_lnl_units_device, inputs resident in HBM), and one RCCL all-reduce of
 the B-vector of partial lnL completes the batch.  Per-GPU work is fixed as N
 grows (weak scaling).  Rank 0 prints ONE JSON line.
+
+Launch contract: `--gpus N` is authoritative.  Started from
+plain `python` with N > 1 and no WORLD_SIZE in the environment, this process
+is a launcher: it runs the CPU baseline (before anything touches a GPU), then
+starts N rank processes of this script (RANK = LOCAL_RANK = r, WORLD_SIZE = N,
+MASTER_ADDR = 127.0.0.1, a free MASTER_PORT) and exits with the first non-zero
+rank status (the other ranks are then terminated).  Started by torchrun
+(WORLD_SIZE set), `--gpus` must equal WORLD_SIZE or the run exits non-zero.
 """
 import argparse
 import json
 import os
+import socket
+import subprocess
 import sys
 import time
 
@@ -228,6 +238,91 @@ def secondary_c5(dev, steps=3, steps_one=20):
     return res
 
 
+def secondary_wide(dev, steps=3):
+    """Bases past the register kernels, where the reference's own rules lead
+    (X_<n>_nfreqs, enterprise_models.py:148-167; determine_nfreqs gives its
+    fake_psr_0 60 frequencies, :457-462; its system_noise_example, :256-338):
+    the 372-column 10k-TOA pulsar with white noise fixed and sampled (B =
+    1024) and the system-noise J1832 model (13 blocks, fixed white noise, B =
+    4096).  Per case, on prior and near-truth draws: ms per batch, evals/s and
+    the share of units the verify step sends to chol_dd_kernel
+    (ewh_refine_stats); the fp64 chol_wide factorisation alone (kernel mode
+    27) against the fp64 MFMA peak (algorithmic m^3/3 + 2 m^2 per unit, m
+    the basis width); every unit in double-double (mode 29); for sampled
+    white noise the contraction (ewh_contract_device) against §8(d)'s
+    contraction flops."""
+    import torch
+    from enterprise_warp_amd import synth
+    ref_examples = os.path.join(ROOT, "tests", "golden", "ref_examples")
+    st = torch.cuda.current_stream(dev)
+    out = {}
+    for name, make in (("w372_fixed", lambda: synth.config_wide(True)),
+                       ("w372_varwn", lambda: synth.config_wide(False)),
+                       ("system", lambda: synth.config_system(ref_examples))):
+        cfg = make()
+        pta, B = cfg.pta, cfg.B
+        eng = pta.engine(device=dev.index)
+        P = len(pta.signal_collections)
+        U = P * B
+        m = np.array([c.T.shape[1] for c in pta.signal_collections])
+        f_chol = float(np.sum(algorithmic_flops_per_unit(m))) * B
+        res = torch.zeros(B, dtype=torch.float64, device=dev)
+
+        def timed(fn, n=steps):
+            fn()
+            torch.cuda.synchronize(dev)
+            a, b = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+            a.record(st)
+            for _ in range(n):
+                fn()
+            b.record(st)
+            torch.cuda.synchronize(dev)
+            return a.elapsed_time(b) / n
+
+        rec = {"batch": B, "columns": int(m.max()), "white_fixed": bool(pta.white_fixed())}
+        draws = (("prior", synth.prior_draws(pta, B, cfg.theta_seed)),
+                 ("near", synth.near_draws(pta, cfg.truth, B, cfg.theta_seed + 1)))
+        for kind, X in draws:
+            th = torch.from_numpy(X).to(dev)
+            run = lambda: eng.lnl_units_device(th.data_ptr(), B, 0, U, res.data_ptr(), st.cuda_stream)  # noqa: E731
+            eng.refine_stats()
+            ms = timed(run)
+            checked, refined = eng.refine_stats()
+            rec[kind] = {"ms_per_batch": ms, "evals_per_s": B / (ms * 1e-3),
+                         "refined_share": refined / checked if checked else None,
+                         "finite_fraction": float(np.mean(np.isfinite(res.cpu().numpy())))}
+            if kind == "prior":
+                eng.set_kernel_mode(27)
+                try:
+                    ms27 = timed(run)
+                finally:
+                    eng.set_kernel_mode(29)
+                try:
+                    ms29 = timed(run, 1)
+                finally:
+                    eng.set_kernel_mode(0)
+                rec["all_fp64_chol_wide"] = {"ms_per_batch": ms27}
+                rec["all_double_double"] = {"ms_per_batch": ms29, "us_per_unit": 1e3 * ms29 / U}
+                if not pta.white_fixed():
+                    cms = timed(lambda: eng.contract_device(th.data_ptr(), B, st.cuda_stream))
+                    fc, by = contraction_work(pta)
+                    rec["contraction"] = {"ms": cms, "fp64_mfma_frac": fc * B / (cms * 1e-3) / 1e12 /
+                                          FP64_MFMA_PEAK_TFLOPS, "flops_per_sample": fc}
+                    ms27 -= cms
+                rec["all_fp64_chol_wide"].update(
+                    factorisation_ms=ms27, fp64_mfma_frac=f_chol / (ms27 * 1e-3) / 1e12 / FP64_MFMA_PEAK_TFLOPS)
+            del th
+        out[name] = rec
+        pta._drop_engine()
+        del res
+    out["note"] = ("prior / near: the default route (verify-and-refine: forward + reversed fp64 chol_wide, "
+                   "chol_dd_kernel on the units whose two orders disagree); refined_share = units refactored "
+                   "in double-double / units on the route; all_fp64_chol_wide = kernel mode 27 (one fp64 "
+                   "factorisation per unit, the contraction subtracted for sampled white noise), fp64_mfma_frac "
+                   "on m^3/3 + 2 m^2 per unit; all_double_double = kernel mode 29")
+    return out
+
+
 def kernel_sources_sha():
     """sha256 of the sources of the factorisation kernel (ewarp_dev.h and its
     instantiating translation unit): ties a committed PMC profile to this tree."""
@@ -269,9 +364,96 @@ def sampler_latency(pta, cfg, batches=(1, 16, 256, 4096), reps=50):
     return out
 
 
+CPU_JSON_ENV = "EWARP_BENCH_CPU_JSON"   # launcher -> rank 0: the CPU baseline it measured
+LAUNCHER_ENV = "EWARP_BENCH_LAUNCHER"   # set in the ranks bench.py itself starts
+
+
+def free_port():
+    with socket.socket() as s:
+        s.bind(("127.0.0.1", 0))
+        return s.getsockname()[1]
+
+
+def rank_environments(n, port, base=None):
+    """Environment of each of the n rank processes the launcher starts: the
+    env:// rendezvous torch.distributed reads (what torchrun would set for one
+    node), one rank per GPU, LOCAL_RANK = RANK."""
+    base = dict(os.environ if base is None else base)
+    envs = []
+    for r in range(n):
+        e = dict(base)
+        e.update(RANK=str(r), LOCAL_RANK=str(r), WORLD_SIZE=str(n), LOCAL_WORLD_SIZE=str(n), GROUP_RANK="0",
+                 MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+        e[LAUNCHER_ENV] = "1"
+        e.pop(CPU_JSON_ENV, None)
+        envs.append(e)
+    return envs
+
+
+def resolve_world(gpus, environ):
+    """(world, launch): the world size of this run and whether this process
+    must start the rank processes itself.  WORLD_SIZE set (torchrun, or our
+    own launcher) wins, but must equal --gpus when that is given; without it,
+    --gpus N > 1 makes this process the launcher."""
+    ws = environ.get("WORLD_SIZE")
+    if ws is not None:
+        ws = int(ws)
+        if gpus is not None and gpus != ws:
+            raise SystemExit(f"bench.py: --gpus {gpus} but WORLD_SIZE={ws}: the launcher and the flag disagree")
+        return ws, False
+    n = 1 if gpus is None else int(gpus)
+    if n < 1:
+        raise SystemExit(f"bench.py: --gpus {n} < 1")
+    return n, n > 1
+
+
+def launch(n, argv, cpu=None, script=None):
+    """Start n rank processes of this script (nothing in this process has
+    touched a GPU), wait for all of them; on the first non-zero exit terminate
+    the others and return that status.  Rank 0 prints the JSON line; the CPU
+    baseline measured here reaches it through a temporary file."""
+    import tempfile
+    envs = rank_environments(n, free_port())
+    tmp = None
+    if cpu is not None:
+        fd, tmp = tempfile.mkstemp(prefix="ewarp_cpu_", suffix=".json")
+        with os.fdopen(fd, "w") as fh:
+            json.dump(cpu, fh)
+        envs[0][CPU_JSON_ENV] = tmp
+    script = os.path.abspath(script or __file__)
+    procs = [subprocess.Popen([sys.executable, script] + list(argv), env=e) for e in envs]
+    rc = 0
+    try:
+        while True:
+            states = [p.poll() for p in procs]
+            bad = [s for s in states if s not in (None, 0)]
+            if bad:
+                rc = bad[0] if bad[0] > 0 else 128 - bad[0]
+                print(f"bench.py launcher: a rank exited with status {bad[0]}; stopping the others",
+                      file=sys.stderr, flush=True)
+                break
+            if all(s == 0 for s in states):
+                break
+            time.sleep(0.1)
+    finally:
+        for p in procs:
+            if p.poll() is None:
+                p.terminate()
+        for p in procs:
+            try:
+                p.wait(timeout=30)
+            except subprocess.TimeoutExpired:
+                p.kill()
+                p.wait()
+        if tmp is not None:
+            os.unlink(tmp)
+    return rc
+
+
 def main():
     ap = argparse.ArgumentParser()
-    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--gpus", type=int, default=None,
+                    help="GPUs (= rank processes) of this run; default WORLD_SIZE, else 1 (see the launch contract)")
     ap.add_argument("--steps", type=int, default=20)
     ap.add_argument("--warmup", type=int, default=3)
     ap.add_argument("--batch-per-gpu", type=int, default=4096)
@@ -281,6 +463,9 @@ def main():
     ap.add_argument("--no-latency", action="store_true")
     ap.add_argument("--no-secondary", action="store_true", help="skip the C2 / C4 / C5 secondary measurements")
     ap.add_argument("--no-c5", action="store_true", help="skip the C5 secondary measurement (~40 s of model build)")
+    ap.add_argument("--no-wide", action="store_true", help="skip the wide-basis secondary measurement")
+    ap.add_argument("--only-wide", action="store_true",
+                    help="measure only the wide-basis secondary block (prints it as one JSON line) and exit")
     ap.add_argument("--kernel-mode", type=int, default=0, help="0 auto (MFMA), 1 LDS fallback")
     ap.add_argument("--config", default="c3", choices=["c3", "c5"],
                     help="c3: the headline 45-pulsar CURN batch (default); c5: 100-pulsar HD-correlated PTA")
@@ -297,21 +482,36 @@ def main():
     args = ap.parse_args()
     if args.same_device and args.dist_backend != "gloo":
         ap.error("--same-device needs --dist-backend gloo (RCCL takes one rank per GPU)")
+    world, spawn = resolve_world(args.gpus, os.environ)
+    if spawn:
+        # launcher: the CPU baseline on this job's cores first, then the ranks
+        cpu = None
+        if args.config == "c3" and not args.no_cpu_baseline:
+            cpu = cpu_baseline(args.cpu_seconds, args.cpu_procs)
+        sys.exit(launch(world, sys.argv[1:], cpu))
     if args.config == "c5":
         return main_c5(args)
+    if args.only_wide:
+        import torch
+        torch.cuda.set_device(0)
+        print(json.dumps({"secondary": {"wide": secondary_wide(torch.device("cuda", 0))}}), flush=True)
+        return
 
     import torch
     import torch.distributed as dist
     from enterprise_warp_amd import sharding, synth
 
-    world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
     # CPU baseline first: worker processes are spawned before this process
-    # initialises the GPU (no forked child ever carries a HIP context)
+    # initialises the GPU (no forked child ever carries a HIP context).  With
+    # N ranks from our launcher it was measured there, on the job's cores
     cpu = None
     if world == 1 and not args.no_cpu_baseline:
         cpu = cpu_baseline(args.cpu_seconds, args.cpu_procs)
+    elif rank == 0 and os.environ.get(CPU_JSON_ENV):
+        with open(os.environ[CPU_JSON_ENV]) as fh:
+            cpu = json.load(fh)
     # --same-device (rehearsal of the multi-rank path on a one-GPU box, with
     # --dist-backend gloo): every rank on cuda:0
     gpu = 0 if (world == 1 or args.same_device) else local
@@ -324,6 +524,9 @@ def main():
     else:
         torch.cuda.set_device(0)
     dev = torch.device("cuda", gpu)
+    rccl_world = dist.get_world_size() if world > 1 else 1
+    if rccl_world != world:
+        raise SystemExit(f"bench.py: the process group has {rccl_world} ranks, --gpus / WORLD_SIZE say {world}")
 
     cfg = synth.config_c3()
     pta = cfg.pta
@@ -333,7 +536,8 @@ def main():
     eng = pta.engine(device=dev.index)
     eng.set_kernel_mode(args.kernel_mode)
     costs = eng.unit_costs()
-    u0, u1 = sharding.unit_ranges(costs, B, world)[rank]
+    ranges = sharding.unit_ranges(costs, B, world)
+    u0, u1 = ranges[rank]
     stream = torch.cuda.current_stream(dev)
     # two output buffers: the all-reduce of step i (RCCL's stream) overlaps
     # the likelihood launch of step i+1 (this stream); step i+2 reuses the
@@ -379,10 +583,13 @@ def main():
     torch.cuda.synchronize(dev)
     elapsed = time.perf_counter() - t0
     launch_ms = float(np.mean([a.elapsed_time(b) for a, b in ev]))
-    t = torch.tensor([elapsed], dtype=torch.float64, device=dev)
+    # every rank's wall time and launch time (the max over ranks is `value`'s clock)
+    t = torch.zeros(2 * world, dtype=torch.float64, device=dev)
+    t[2 * rank], t[2 * rank + 1] = elapsed, launch_ms
     if world > 1:
-        dist.all_reduce(t, op=dist.ReduceOp.MAX)
-    elapsed = float(t.item())
+        dist.all_reduce(t)
+    per_rank = t.cpu().numpy().reshape(world, 2)
+    elapsed = float(per_rank[:, 0].max())
     lnl = outs[(args.steps - 1) & 1].cpu().numpy()
     verify = None
     if args.verify and rank == 0:
@@ -426,6 +633,8 @@ def main():
         secondary = secondary_configs(dev)
         if not args.no_c5:
             secondary["c5"] = secondary_c5(dev)
+        if not args.no_wide:
+            secondary["wide"] = secondary_wide(dev)
     if rank == 0:
         value = B * args.steps / elapsed
         rec = {
@@ -437,6 +646,12 @@ def main():
                                    "CURN 14 freqs merged, fixed white noise (TNT cached), basis m=132",
                        "global_batch": B, "batch_per_gpu": args.batch_per_gpu, "n_pulsars": len(m_psr),
                        "parallelism": f"units{world}", "finite_fraction": float(np.mean(np.isfinite(lnl)))},
+            "rccl_world": rccl_world,
+            "dist": {"backend": args.dist_backend if world > 1 else None, "same_device": bool(args.same_device),
+                     "launcher": "bench.py" if os.environ.get(LAUNCHER_ENV) else
+                     ("torchrun" if os.environ.get("TORCHELASTIC_RUN_ID") else None),
+                     "unit_ranges": [list(r) for r in ranges],
+                     "rank_elapsed_s": per_rank[:, 0].tolist(), "rank_launch_ms": per_rank[:, 1].tolist()},
             "roofline": {"bound": "mfma", "achieved": achieved, "peak": FP64_MFMA_PEAK_TFLOPS, "unit": "TFLOP/s",
                          "frac": achieved / FP64_MFMA_PEAK_TFLOPS, "traffic": traffic, "traffic_source": traffic_src,
                          "kernel": "chol_mfma_kernel<8,2,25> (two-level blocked LDL^T panel: 4-row sub-panels by "
@@ -449,10 +664,9 @@ def main():
             rec["secondary"] = secondary
         if cpu is not None:
             rec["cpu_baseline"] = cpu
-            rec["gpu_over_cpu"] = {"per_gpu": value / world / cpu["value"],
-                                   "note": "one GPU against the CPU cores this job is given (its node share); "
-                                           "a whole node is 8 such shares, so the node-level ratio at perfect "
-                                           "scaling is the same figure (SCALE_rNN measures the real curve)"}
+            rec["gpu_over_cpu"] = {"per_gpu": value / world / cpu["value"], "job": value / cpu["value"],
+                                   "note": f"job = this run's {world} GPU(s) against the {cpu['cores']} CPU cores "
+                                           f"the same job is given (measured in this run); per_gpu = job / {world}"}
         if latency is not None:
             rec["sampler_latency"] = latency
         if verify is not None:
@@ -474,12 +688,16 @@ def main_c5(args):
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
+    gpu = 0 if (world == 1 or args.same_device) else local
+    torch.cuda.set_device(gpu)
     if world > 1:
-        torch.cuda.set_device(local)
-        dist.init_process_group("nccl", device_id=torch.device("cuda", local))
-    else:
-        torch.cuda.set_device(0)
-    dev = torch.device("cuda", local if world > 1 else 0)
+        if args.dist_backend == "nccl":
+            dist.init_process_group("nccl", device_id=torch.device("cuda", gpu))
+        else:
+            dist.init_process_group(args.dist_backend)
+        if dist.get_world_size() != world:
+            raise SystemExit(f"bench.py: the process group has {dist.get_world_size()} ranks, WORLD_SIZE {world}")
+    dev = torch.device("cuda", gpu)
     cfg = synth.config_c5()
     pta = cfg.pta
     if args.partition == "pulsars":
@@ -520,7 +738,7 @@ def main_c5(args):
     achieved = flops * args.steps / elapsed / 1e12
     if rank == 0:
         rec = {"metric": "lnL evals/sec (whole node), 100-psr HD-correlated PTA (BASELINE config 5)",
-               "value": Bg * world * args.steps / elapsed, "unit": "lnL evals/s", "n_gpus": world,
+               "value": Bg * world * args.steps / elapsed, "unit": "lnL evals/s", "n_gpus": world, "rccl_world": world,
                "steps": args.steps, "warmup": args.warmup, "ms_per_step": 1e3 * elapsed / args.steps,
                "higher_is_better": True, "scaling": "weak", "vs_baseline": None, "dtype": "f64",
                "data": "synthetic: seeded 100-pulsar x 20k-TOA PTA, HD GWB 14 freqs (SURVEY.md §8(d) C5)",
@@ -587,7 +805,8 @@ def c5_pulsar_partition(args, cfg, world, rank, dev):
     lnl = out.cpu().numpy()
     if rank == 0:
         rec = {"metric": "lnL evals/sec, 100-psr HD-correlated PTA, pulsar-partitioned (BASELINE config 5)",
-               "value": B * args.steps / elapsed, "unit": "lnL evals/s", "n_gpus": world, "steps": args.steps,
+               "value": B * args.steps / elapsed, "unit": "lnL evals/s", "n_gpus": world, "rccl_world": world,
+               "steps": args.steps,
                "warmup": args.warmup, "ms_per_step": 1e3 * elapsed / args.steps, "higher_is_better": True,
                "scaling": "strong", "vs_baseline": None, "dtype": "f64",
                "data": "synthetic: seeded 100-pulsar x 20k-TOA PTA, HD GWB 14 freqs (SURVEY.md §8(d) C5)",

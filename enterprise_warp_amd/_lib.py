@@ -62,7 +62,7 @@ class PtaDesc(C.Structure):
 EXPORTS = ["ewh_create", "ewh_num_devices", "ewh_set_fixed_white", "ewh_lnl_batch", "ewh_lnl_units_device",
            "ewh_keep_dim", "ewh_corr_partial_device", "ewh_corr_finish_device",
            "ewh_last_unit_terms", "ewh_unit_cost", "ewh_set_kernel_mode", "ewh_optstat", "ewh_contract_device",
-           "ewh_transfer_stats",
+           "ewh_transfer_stats", "ewh_lat_b_max", "ewh_refine_stats",
            "ewh_destroy", "ewh_last_error", "ewh_version"]
 DEV_EXPORTS = ["ewh_dev_gram", "ewh_dev_reduced"]
 
@@ -122,6 +122,10 @@ def load():
     lib.ewh_contract_device.restype = C.c_int
     lib.ewh_transfer_stats.argtypes = [C.c_void_p, C.POINTER(C.c_int64), C.POINTER(C.c_int64)]
     lib.ewh_transfer_stats.restype = C.c_int
+    lib.ewh_refine_stats.argtypes = [C.c_void_p, C.POINTER(C.c_int64), C.POINTER(C.c_int64)]
+    lib.ewh_refine_stats.restype = C.c_int
+    lib.ewh_lat_b_max.argtypes = []
+    lib.ewh_lat_b_max.restype = C.c_int
     lib.ewh_destroy.argtypes = [C.c_void_p]
     lib.ewh_destroy.restype = None
     lib.ewh_last_error.argtypes = []

@@ -128,23 +128,27 @@ __global__ __launch_bounds__(256) void chol_dd_kernel(const CholJob* __restrict_
 // term (and on -inf), or the unit goes to the list for chol_dd_kernel.
 __global__ __launch_bounds__(256) void verify_units_kernel(const double* __restrict__ a, const double* __restrict__ b,
                                                            long long u0, long long n, int* __restrict__ list,
-                                                           int* __restrict__ count) {
+                                                           int* __restrict__ count, int* __restrict__ total) {
   const long long i = (long long)blockIdx.x * 256 + threadIdx.x;
+  if (total && i == 0) atomicAdd(total + 1, (int)n);     // (ewh_refine_stats: units checked)
   if (i >= n) return;
   const long long u = u0 + i;
   const double x = a[u], y = b[u];
   const bool fx = x - x == 0.0, fy = y - y == 0.0;           // finite
   const bool bad = (fx != fy) || (fx && fabs(x - y) > 0.25 * (1e-6 + 1e-10 * fabs(x)));
-  if (bad) list[atomicAdd(count, 1)] = (int)u;
+  if (bad) {
+    list[atomicAdd(count, 1)] = (int)u;
+    if (total) atomicAdd(total, 1);       // (ewh_refine_stats: units refined)
+  }
 }
 
 }  // namespace
 
 int launch_verify_units(const double* a, const double* b, long long u0, long long n, int* list, int* count,
-                        hipStream_t st) {
+                        int* total, hipStream_t st) {
   if (n <= 0) return 0;
   hipLaunchKernelGGL(verify_units_kernel, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, st, a, b, u0, n, list,
-                     count);
+                     count, total);
   const hipError_t e = hipGetLastError();
   return e == hipSuccess ? 0 : set_err(EWH_E_HIP, std::string("verify_units_kernel: ") + hipGetErrorString(e));
 }

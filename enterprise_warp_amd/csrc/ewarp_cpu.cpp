@@ -257,6 +257,7 @@ void refresh_fixed(ewh_handle* H) {
 extern "C" {
 
 int ewh_version(void) { return EWH_ABI_VERSION; }
+int ewh_lat_b_max(void) { return 0; }   // no latency kernel on the host
 
 const char* ewh_last_error(void) { return g_err.c_str(); }
 
@@ -358,6 +359,13 @@ int ewh_lnl_batch(ewh_handle* H, const double* theta, int32_t B, double* out) {
 int ewh_last_unit_terms(ewh_handle* H, double* out, int32_t B) {
   if (!H || !out || B != H->last_B) return set_err(EWH_E_INVALID, "bad arguments / B differs from the last call");
   std::memcpy(out, H->units.data(), sizeof(double) * H->units.size());
+  return 0;
+}
+
+int ewh_refine_stats(ewh_handle* H, int64_t* checked, int64_t* refined) {
+  if (!H) return set_err(EWH_E_INVALID, "bad handle");
+  if (checked) *checked = 0;     // (no double-double route on the host: the twin factors in double)
+  if (refined) *refined = 0;
   return 0;
 }
 

@@ -1443,9 +1443,10 @@ int launch_chol_dd(const CholJob* jobs, int B, long long u0, long long n, int b_
                    double* units, double* scr, long long scr_per_wg, long long cap, hipStream_t st);
 // the verify-and-refine form: units a (forward fp64) vs b (reversed fp64) of
 // [u0, u0 + n) -> list / count of the disagreeing ones (count zeroed by the
-// caller), then chol_dd_kernel over the list (cap workgroups looping) into units
+// caller; total, if not NULL: total[0] += the count, total[1] += n), then
+// chol_dd_kernel over the list (cap workgroups looping) into units
 int launch_verify_units(const double* a, const double* b, long long u0, long long n, int* list, int* count,
-                        hipStream_t st);
+                        int* total, hipStream_t st);
 int launch_chol_dd_list(const CholJob* jobs, int B, int b_off, const double* theta, int ldth, double* units,
                         double* scr, long long scr_per_wg, long long cap, const int* list, const int* count,
                         hipStream_t st);

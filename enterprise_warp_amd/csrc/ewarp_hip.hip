@@ -1416,6 +1416,11 @@ struct DevCtx {
   size_t units2_cap = 0;
   int* d_ddlist = nullptr;       // the verify step's flagged units, [0] = count, list from [1]
   size_t ddlist_cap = 0;
+  // ewh_refine_stats since the last query: device counters [0] units
+  // chol_dd_kernel refactored, [1] units verified (counted by the verify
+  // kernel, so graph replays count too); MODE_DD's units on the host
+  int* d_ddstat = nullptr;
+  long long dd_forced = 0;
   double* d_Glo = nullptr;       // varying white noise, bases past 16 blocks: the low part of G (contract_wide_kernel)
   int chunk = 0;
   int chunk_cap = 0;          // largest chunk the ~1.5 GB scratch budget allows
@@ -1696,9 +1701,15 @@ int launch_dd_path(DevCtx* h, int nb, const CholJob* jobs, int B, long long u0, 
   const long long cap = ensure_dd_scratch(h, 16 * nb);
   if (cap <= 0) return EWH_E_NOMEM;
   const long long per = dd_scratch_per_wg(16 * nb);
-  if (h->kernel_mode == MODE_DD)
+  if (h->kernel_mode == MODE_DD) {
+    h->dd_forced += n;
     return launch_chol_dd(jobs, B, u0, n, b_off, theta, ldth, units, h->d_ddscr, per, cap, st);
+  }
   int rc;
+  if (!h->d_ddstat) {
+    if ((rc = dalloc(h, &h->d_ddstat, 2))) return rc;
+    EWH_HIP(hipMemsetAsync(h->d_ddstat, 0, 2 * sizeof(int), st));
+  }
   const size_t U = (size_t)(h->P + (h->corr ? 1 : 0)) * B;
   if ((rc = ensure_buf(h, &h->d_units2, &h->units2_cap, U)) || (rc = ensure_buf(h, &h->d_ddlist, &h->ddlist_cap, U + 1)))
     return rc;
@@ -1706,7 +1717,7 @@ int launch_dd_path(DevCtx* h, int nb, const CholJob* jobs, int B, long long u0, 
       (rc = launch_wide(h, nb, 0, jobs, B, u0, n, b_off, theta, ldth, h->d_units2, nullptr, st, 1)))
     return rc;
   EWH_HIP(hipMemsetAsync(h->d_ddlist, 0, sizeof(int), st));
-  if ((rc = launch_verify_units(units, h->d_units2, u0, n, h->d_ddlist + 1, h->d_ddlist, st))) return rc;
+  if ((rc = launch_verify_units(units, h->d_units2, u0, n, h->d_ddlist + 1, h->d_ddlist, h->d_ddstat, st))) return rc;
   return launch_chol_dd_list(jobs, B, b_off, theta, ldth, units, h->d_ddscr, per, std::min<long long>(cap, n),
                              h->d_ddlist + 1, h->d_ddlist, st);
 }
@@ -3098,6 +3109,7 @@ int lnl_batch_single(ewh_handle* H, DevCtx* h, int B, double* out_host) {
 extern "C" {
 
 int ewh_version(void) { return EWH_ABI_VERSION; }
+int ewh_lat_b_max(void) { return LAT_B_MAX; }
 
 const char* ewh_last_error(void) { return g_err.c_str(); }
 
@@ -3178,6 +3190,26 @@ int ewh_transfer_stats(const ewh_handle* H, int64_t* h2d_bytes, int64_t* peer) {
   if (!H) return set_err(EWH_E_INVALID, "bad handle");
   if (h2d_bytes) *h2d_bytes = H->h2d_bytes;
   if (peer) *peer = H->peer_mask;
+  return 0;
+}
+
+int ewh_refine_stats(ewh_handle* H, int64_t* checked, int64_t* refined) {
+  if (!H) return set_err(EWH_E_INVALID, "bad handle");
+  long long c = 0, r = 0;
+  for (DevCtx* h : H->ctx) {
+    EWH_HIP(hipSetDevice(h->device));
+    EWH_HIP(hipStreamSynchronize(h->stream));
+    int v[2] = {0, 0};
+    if (h->d_ddstat) {
+      EWH_HIP(hipMemcpy(v, h->d_ddstat, 2 * sizeof(int), hipMemcpyDeviceToHost));
+      EWH_HIP(hipMemset(h->d_ddstat, 0, 2 * sizeof(int)));
+    }
+    c += h->dd_forced + v[1];
+    r += h->dd_forced + v[0];
+    h->dd_forced = 0;
+  }
+  if (checked) *checked = c;
+  if (refined) *refined = r;
   return 0;
 }
 

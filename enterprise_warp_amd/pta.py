@@ -399,13 +399,17 @@ class Engine:
         # sampler-sized calls (one theta per call: PTMCMC / bilby) go through
         # persistent buffers whose addresses are bound once -- building two
         # ctypes pointers per call costs ~5 us, a tenth of the call
+        # the latency kernel's batch bound, from the library (LAT_B_MAX)
+        self.SMALL_B = max(1, int(self.lib.ewh_lat_b_max()))
         self._small = np.empty((self.SMALL_B, max(1, self.n_param)))
         self._small_out = np.empty(self.SMALL_B)
         self._small_fn = C.CFUNCTYPE(C.c_int, C.c_void_p, C.c_void_p, C.c_int32, C.c_void_p)(
             ("ewh_lnl_batch", self.lib))
         self._small_args = (self.h, self._small.ctypes.data, self._small_out.ctypes.data)
 
-    SMALL_B = 24     # (the latency kernel's batch bound, LAT_B_MAX in csrc/ewarp_hip.hip)
+    def lat_b_max(self):
+        """The latency path's batch bound (ewh_lat_b_max; 0: none)."""
+        return int(self.lib.ewh_lat_b_max())
 
     def lnl_batch(self, theta):
         theta = np.ascontiguousarray(theta, dtype=float)
@@ -508,6 +512,13 @@ class Engine:
         b, m = C.c_int64(), C.c_int64()
         _lib.check(self.lib.ewh_transfer_stats(self.h, C.byref(b), C.byref(m)))
         return int(b.value), int(m.value)
+
+    def refine_stats(self):
+        """(units on the double-double route, units chol_dd_kernel refactored)
+        since the last query -- ewh_refine_stats (synchronises, resets)."""
+        c, r = C.c_int64(), C.c_int64()
+        _lib.check(self.lib.ewh_refine_stats(self.h, C.byref(c), C.byref(r)))
+        return int(c.value), int(r.value)
 
     def unit_costs(self):
         return np.array([self.lib.ewh_unit_cost(self.h, p) for p in range(self.n_pulsar)])

@@ -344,3 +344,39 @@ def config_c1(data_dir, noise_json=None, seed=1832):
     truth = {k.replace("_log10_equad", "_log10_tnequad"): v for k, v in nd.items()}
     simulate_residuals(pta, truth, seed)
     return SimpleNamespace(name="C1", pta=pta, truth=truth, B=64, theta_seed=seed)
+
+
+def config_wide(fixed_white, n_toa=10000, nfreqs=60, seed=60):
+    """A basis past every register kernel at a realistic size: one pulsar of
+    10k TOAs with red / DM / chromatic noise at 60 frequencies each
+    (X_60_nfreqs, enterprise_models.py:148-167; the reference's own
+    determine_nfreqs gives its fake_psr_0 60, :457-462): 12 + 360 columns,
+    24 blocks.  White noise fixed (the cached Gram) or sampled."""
+    psr = make_pulsar("J0000+0060", n_toa, seed=seed, epoch_size=16)
+    terms = {"efac": "by_backend", "equad": "by_backend", "ecorr": "by_backend",
+             "spin_noise": f"powerlaw_{nfreqs}_nfreqs", "dm_noise": f"powerlaw_{nfreqs}_nfreqs",
+             "chromred": f"4_{nfreqs}_nfreqs"}
+    wn = white_noisedict([psr], seed + 1)
+    ns = params_namespace(psr.toas.max() - psr.toas.min(), fixed_white)
+    pta = build_pta([psr], terms, {}, ns, wn if fixed_white else None)
+    truth = truth_values(pta, seed + 2, white=wn)
+    simulate_residuals(pta, truth, seed + 3)
+    return SimpleNamespace(name="wide", pta=pta, truth=truth, B=1024, theta_seed=seed + 5, terms=terms)
+
+
+def config_system(data_dir, seed=8):
+    """The reference's system_noise_example.dat / system_noise_example.json on
+    J1832-0836 (data_dir: a copy of its examples/ tree): efac / equad fixed,
+    spin + DM noise, system noise on the PDFB_40CM and CASPSR_40CM groups,
+    band noise on 10CM (enterprise_models.py:256-338) -- 13 blocks with fixed
+    white noise.  The model of the golden fixture c1_system."""
+    c1 = config_c1(data_dir)
+    psr = c1.pta.signal_collections[0].psr
+    ns = params_namespace(np.ptp(psr.toas), True)
+    terms = {"efac": "by_backend", "equad": "by_backend", "spin_noise": "powerlaw", "dm_noise": "powerlaw",
+             "system_noise": ["PDFB_40CM", "CASPSR_40CM"], "ppta_band_noise": ["10CM"]}
+    wn = {k: v for k, v in c1.truth.items() if k.endswith("_efac") or k.endswith("_log10_tnequad")}
+    pta = build_pta([psr], terms, {}, ns, wn)
+    truth = truth_values(pta, seed, white=wn)
+    simulate_residuals(pta, truth, seed + 1)
+    return SimpleNamespace(name="system", pta=pta, truth=truth, B=4096, theta_seed=19, terms=terms)

@@ -260,12 +260,22 @@ double ewh_unit_cost(const ewh_handle* h, int32_t pulsar);
  * on the first device set their bit too.  Either pointer may be NULL. */
 int ewh_transfer_stats(const ewh_handle* h, int64_t* h2d_bytes, int64_t* peer);
 
+/* The double-double route since the last query (bases past the register
+ * kernels: fixed white noise past 9 blocks, any basis past 16):
+ * *checked = units that took it, *refined = units chol_dd_kernel refactored
+ * (the verify step flagged them -- the forward and reversed fp64
+ * factorisations disagree by more than a quarter of strict -- or kernel mode
+ * 29 sent every unit; those are counted at launch, so not in replays of a
+ * captured ewh_lnl_batch graph).  Synchronises the handle's streams and
+ * resets both counts.  Either pointer may be NULL.  (Host twin: always 0.) */
+int ewh_refine_stats(ewh_handle* h, int64_t* checked, int64_t* refined);
+
 /* Kernel selection: 0 = auto (register-blocked MFMA factorisation with the
  * two-level LDL^T panel -- the 16x16 diagonal block in 4-row sub-panels by
  * VALU, each closed by one symmetric MFMA rank-4 update, the rest of the
  * block row by MFMA with L^-1 -- when the matrix fits registers; the LDS
- * kernel otherwise; batches of up to 8 samples on one device take the
- * latency kernel, one 4-wave workgroup per (pulsar, sample) with theta read
+ * kernel otherwise; batches of up to ewh_lat_b_max() = 24 samples on one
+ * device take the latency kernel, one 4-wave workgroup per (pulsar, sample) with theta read
  * from pinned memory and the unit terms written to pinned memory, folded by
  * the host), 2 = the default without
  * that latency path (batched kernels at every batch size), 1 = force the
@@ -298,6 +308,12 @@ int ewh_transfer_stats(const ewh_handle* h, int64_t* h2d_bytes, int64_t* peer);
  * each diagonal block factored in a launch of its own instead of inside the
  * previous trailing update.  Other modes return EWH_E_UNSUPPORTED. */
 int ewh_set_kernel_mode(ewh_handle* h, int32_t mode);
+
+/* The largest batch the single-launch latency path serves (LAT_B_MAX; a
+ * fixed-white-noise uncorrelated / CURN batch of at most this many samples on
+ * one device is one launch of chol_lat_kernel).  0: no latency path (the host
+ * twin).  Callers size their persistent small-batch buffers from it. */
+int ewh_lat_b_max(void);
 
 void ewh_destroy(ewh_handle* h);
 const char* ewh_last_error(void);

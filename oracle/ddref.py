@@ -17,6 +17,8 @@ the power laws through mpmath at 40 digits); the timing-model columns and
 everything else are factored together, as enterprise does, by an unblocked
 double-double Cholesky; log d_k = log(hi) + lo/hi.
 """
+import math
+
 import mpmath
 import numpy as np
 
@@ -98,6 +100,19 @@ def dd_gram(X, w):
     return dd_add(acc, dd_of(A_lo.T @ X))
 
 
+def dd_matmul_tn(A, B):
+    """A^T B for double-double matrices (hi, lo): A_hi^T B_hi error free
+    (18-bit slices, as dd_gram), A_hi^T B_lo + A_lo^T B_hi by fp64 products
+    (2^-53-relative terms of a 2^-53-relative correction)."""
+    SA, SB = _slices(A[0]), _slices(B[0])
+    k = len(SA)
+    acc = (np.zeros((A[0].shape[1], B[0].shape[1])), np.zeros((A[0].shape[1], B[0].shape[1])))
+    for s in range(k):
+        for t in range(k - s):
+            acc = dd_add(acc, dd_of(SA[s].T @ SB[t]))
+    return dd_add(acc, dd_of(A[0].T @ B[1] + A[1].T @ B[0]))
+
+
 def pow10_dd(x):
     return dd_from_mp(mpmath.power(10, 2 * mpmath.mpf(float(x))))
 
@@ -143,6 +158,7 @@ class DDReferencePTA:
         if self.o.correlated():
             raise ValueError("DDReferencePTA: uncorrelated / CURN models only")
         self.pulsars = self.o.pulsars
+        self._gram_cache = {}
 
     def _white(self, pp, p):
         """N diagonal (double-double) and the ECORR epochs (slice, J)."""
@@ -182,27 +198,55 @@ class DDReferencePTA:
     def pulsar_terms(self, pp, p):
         T = np.asarray(pp.basis({k: float(v) for k, v in p.items() if np.ndim(v) == 0}), float)
         X = np.concatenate([T, np.asarray(pp.r, float)[:, None]], axis=1)
+        # the Gram and log|N| depend on theta only through the white-noise
+        # parameters and a sampled chromatic index: cached on those values
+        # (enterprise caches TNT the same way), so fixed white noise forms it once
+        key = (id(pp), tuple(float(p[nm]) for _, _, names in pp.white for nm in sorted(names.values())),
+               tuple(float(p[pn]) for _, _, pn in pp.basis_params))
+        if key in self._gram_cache:
+            G, ldn = self._gram_cache[key]
+        else:
+            G, ldn = self._gram(pp, p, X)
+            self._gram_cache[key] = (G, ldn)
+            if len(self._gram_cache) > 16:
+                self._gram_cache.pop(next(iter(self._gram_cache)))
+        return self._factor(pp, p, G, ldn)
+
+    def _gram(self, pp, p, X):
         m1 = X.shape[1]
         D, ep = self._white(pp, p)
         one = (np.ones_like(D[0]), np.zeros_like(D[0]))
         w = dd_div(one, D)
         G = dd_gram(X, w)
-        ldn = float(np.sum(dd_log(D)))
-        for slc, J in ep:
-            wi = (w[0][slc], w[1][slc])
-            sw = (np.float64(0.0), np.float64(0.0))
-            for t in range(len(wi[0])):
-                sw = dd_add(sw, (wi[0][t], wi[1][t]))
-            Jd = (np.float64(J[0]), np.float64(J[1]))
-            beta = dd_div((np.float64(1.0), np.float64(0.0)), dd_add(sw, dd_div((np.float64(1.0), np.float64(0.0)), Jd)))
-            sv = (np.zeros(m1), np.zeros(m1))
-            Xs = X[slc]
-            for t in range(Xs.shape[0]):
-                sv = dd_add(sv, dd_mul((Xs[t], np.zeros(m1)), (np.full(m1, wi[0][t]), np.full(m1, wi[1][t]))))
-            outer = dd_mul((sv[0][:, None] * np.ones(m1)[None, :], sv[1][:, None] * np.ones(m1)[None, :]),
-                           (sv[0][None, :] * np.ones(m1)[:, None], sv[1][None, :] * np.ones(m1)[:, None]))
-            G = dd_add(G, dd_neg(dd_mul(outer, (np.full((m1, m1), beta[0]), np.full((m1, m1), beta[1])))))
-            ldn += float(dd_log(Jd) - dd_log(beta))
+        ldn = math.fsum(dd_log(D))
+        if ep:
+            # every epoch at once: rows t = 0.. of all epochs summed together
+            # (epochs hold few TOAs), products exact by TwoProduct
+            E = len(ep)
+            lens = np.array([slc.stop - slc.start for slc, _ in ep])
+            L = int(lens.max())
+            rows = np.array([slc.start for slc, _ in ep])[:, None] + np.arange(L)[None, :]
+            valid = np.arange(L)[None, :] < lens[:, None]
+            rows = np.where(valid, rows, 0)
+            wh, wl = np.where(valid, w[0][rows], 0.0), np.where(valid, w[1][rows], 0.0)
+            sw = (np.zeros(E), np.zeros(E))
+            sv = (np.zeros((E, m1)), np.zeros((E, m1)))
+            for t in range(L):
+                sw = dd_add(sw, (wh[:, t], wl[:, t]))
+                Xt = X[rows[:, t]]
+                sv = dd_add(sv, dd_mul((Xt, np.zeros_like(Xt)), (wh[:, t:t + 1] * np.ones(m1), wl[:, t:t + 1] * np.ones(m1))))
+            one_e = (np.ones(E), np.zeros(E))
+            Jd = (np.array([J[0] for _, J in ep]), np.array([J[1] for _, J in ep]))
+            beta = dd_div(one_e, dd_add(sw, dd_div(one_e, Jd)))
+            # G -= sum_e beta_e s_e s_e^T = A^T S with A = beta (.) S: the
+            # hi x hi product error free (slices), the hi x lo cross terms in fp64
+            A = dd_mul(sv, (beta[0][:, None] * np.ones(m1), beta[1][:, None] * np.ones(m1)))
+            G = dd_add(G, dd_neg(dd_matmul_tn(A, sv)))
+            ldn = math.fsum(np.concatenate(([ldn], dd_log(Jd), -dd_log(beta))))
+        return G, ldn
+
+    def _factor(self, pp, p, G, ldn):
+        m1 = G[0].shape[0]
         phiinv, lphi = self._phi(pp, p)
         Gh, Gl = G[0].copy(), G[1].copy()
         idx = np.arange(m1 - 1)

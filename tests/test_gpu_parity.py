@@ -307,3 +307,55 @@ def test_ptmcmc_fixed_white_latency_path(require_gpu, tmp_path):
     npar = len(pta.param_names)
     want = oracle_lnl(pta, rows[:, :npar])
     check_parity(rows[:, npar + 1], want, "PTMCMC on c3_small (latency kernel) logged lnL")
+
+
+def wide_model(fixed_white):
+    cfg = synth.config_wide(fixed_white)
+    return cfg.pta, cfg.truth
+
+
+def _route_vs_dd(pta, X, got, label):
+    """The default route (two fp64 chol_wide orders verify each other, the
+    disagreeing units refactored in double-double) against kernel mode 29
+    (every unit in double-double): strict on every sample.  This is the
+    verify heuristic's blind spot -- two fp64 orders that agree and are both
+    wrong would pass the verify and fail here."""
+    eng = pta.engine()
+    eng.set_kernel_mode(29)
+    try:
+        dd = pta.get_lnlikelihood_batch(X)
+    finally:
+        eng.set_kernel_mode(0)
+    check_parity(got, dd, label + ": default route vs double-double everywhere")
+
+
+@pytest.mark.parametrize("fixed_white", [True, False])
+def test_wide_prior_draws_full_size(require_gpu, fixed_white):
+    """The route that exists for prior draws, at a realistic size: the first
+    8 prior draws of the 372-column, 10k-TOA model (white noise fixed: the
+    double-double S of gram_dd + schur; sampled: contract_wide_kernel's
+    G_hi + G_lo), each sample no less accurate than enterprise's fp64 order
+    against the double-double reference (oracle/ddref.py), and the default
+    route equal to double-double everywhere at strict.  The call matched is
+    pta.get_lnlikelihood (bilby_warp.py:35)."""
+    pta, _ = wide_model(fixed_white)
+    X = synth.prior_draws(pta, 8, 65)
+    got = pta.get_lnlikelihood_batch(X)
+    ent, ext = reference_lnl(pta, X, exact="dd")
+    label = f"wide 372 columns prior draws, fixed white {fixed_white}"
+    check_accuracy(got, ent, ext, label, per_sample=True)
+    _route_vs_dd(pta, X, got, label)
+
+
+def test_system_noise_prior_draws(require_gpu):
+    """The reference's system_noise_example model on J1832-0836
+    (enterprise_models.py:256-338: system noise on two groups + band noise,
+    fixed white noise; 13 blocks -> verify-and-refine): 16 fresh prior draws,
+    per-sample accuracy against the double-double reference, and the default
+    route equal to double-double everywhere at strict."""
+    pta, _, _, _ = load_golden("c1_system")
+    X = synth.prior_draws(pta, 16, 1832)
+    got = pta.get_lnlikelihood_batch(X)
+    ent, ext = reference_lnl(pta, X, exact="dd")
+    check_accuracy(got, ent, ext, "c1_system model, 16 prior draws", per_sample=True)
+    _route_vs_dd(pta, X, got, "c1_system model, 16 prior draws")

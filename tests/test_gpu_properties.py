@@ -107,11 +107,13 @@ def test_multi_context_handle(require_gpu, name):
 
 def test_multi_context_theta_staging(require_gpu):
     """A handle spanning a node's contexts sends each context only the theta
-    entries its units read (ewh_transfer_stats): C3's model on 16 pulsars over
-    8 contexts -- the per-pulsar columns once in total, the shared CURN
-    columns once per context -- at most 1.2 x B x n_param x 8 bytes per
-    batch, with the per-pulsar terms bit-identical to one context and peer
-    access recorded for every context."""
+    entries its units read (ewh_transfer_stats): C3's model on 45 pulsars
+    (300-1200 TOAs) over 8 contexts -- the per-pulsar columns once in total,
+    the shared CURN columns once per context -- at most 1.2 x B x n_param x 8
+    bytes per batch, with the per-pulsar terms bit-identical to one context
+    and peer access recorded for every context.  The bound needs P >> 2 ndev:
+    each context boundary that splits a pulsar sends that pulsar's columns
+    twice, and the 2 CURN columns go to every context (16 pulsars: 1.21 x)."""
     c3s = synth.config_c3(n_psr=45, n_min=300, n_max=1200, epoch_size=8)
     pta = c3s.pta
     B = 256
@@ -216,22 +218,25 @@ def test_correlated_pulsar_partition(require_gpu):
 
 @pytest.mark.parametrize("name", ["c3_small", "c3_freesp", "c1_j1832", "c1_system", "full_c3"])
 def test_latency_kernel_matches_batched(require_gpu, c3, name):
-    """Batches of up to 8 samples on one device run chol_lat_kernel (one
-    4-wave workgroup per unit, theta read from pinned memory, the pulsar fold
-    and the lnL write fused into the launch).  Its factor, pivots and q are
-    the batched kernel's bit for bit; only the log-determinant sum is
-    associated differently, so lnL must agree with the batched path (kernel
-    mode 2: latency path off) far inside the strict bound, with the same -inf
-    pattern, for B = 1 (a sampler's single proposal), 5 and 8."""
+    """Batches of up to 24 samples (LAT_B_MAX) on one device run
+    chol_lat_kernel (one 4-wave workgroup per unit, theta read from pinned
+    memory, the pulsar fold and the lnL write fused into the launch).  Its
+    factor, pivots and q are the batched kernel's bit for bit; only the
+    log-determinant sum is associated differently, so lnL must agree with the
+    batched path (kernel mode 2: latency path off) far inside the strict
+    bound, with the same -inf pattern, for B = 1 (a sampler's single
+    proposal), 5, 8, 12, 16 and 24 (the bound)."""
     from conftest import load_golden
     if name == "full_c3":
         pta = c3.pta
-        X = np.vstack([synth.prior_draws(pta, 8, 45), synth.near_draws(pta, c3.truth, 8, 3)])
+        X = np.vstack([synth.prior_draws(pta, 12, 45), synth.near_draws(pta, c3.truth, 12, 3)])
     else:
         pta, X, _, _ = load_golden(name)
+        X = np.vstack([X, X[::-1]])                     # 32 rows (16 golden samples, each twice)
     eng = pta.engine()
+    assert eng.lat_b_max() == 24
     worst = 0.0
-    for B in (1, 5, 8):
+    for B in (1, 5, 8, 12, 16, 24):
         XX = X[:B]
         eng.set_kernel_mode(2)
         ref = pta.get_lnlikelihood_batch(XX)
@@ -273,7 +278,7 @@ def test_correlated_right_looking_small_chunks(require_gpu):
 def test_correlated_row_pairs_bit_identical(require_gpu, n_psr):
     """Chunks of >= 64 samples update two block rows of Sigma_c per pass
     (dchol_rowpair_kernel: rows k, k + 1 take every p < k together, row
-    k + 1 then p = k); chunks of <= 4 factor right-looking.  Per tile the
+    k + 1 then p = k); chunks of <= 12 factor right-looking.  Per tile the
     same K = 64 slabs in the same order: bit-identical lnL.  16 pulsars: 8
     block rows (the last pair ends the matrix), 20 pulsars: 9 (a single last
     row)."""
