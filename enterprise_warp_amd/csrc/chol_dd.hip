@@ -15,17 +15,30 @@
 // G_lo), so the factorisation in double-double leaves the lnL within ~1
 // strict of the exact value.
 //
-// One 256-thread workgroup per (pulsar, sample): the n x n matrix (upper
-// triangle used, r last) as hi / lo planes in a per-workgroup scratch, phi^-1
-// added to the diagonal in double-double, then a right-looking LDL^T: per
-// pivot k the row k and the multipliers w_j = A_kj / d_k staged in LDS, the
-// trailing upper triangle A_ij -= A_ki w_j (wave w: rows i = k+1+w, +4, ...;
-// lanes: columns) in double-double; log d_k summed per pivot; the last pivot
-// is q = r^T N^-1 r - d^T Sigma^-1 d.
+// Blocked right-looking Cholesky, one 512-thread workgroup per (pulsar,
+// sample); the trailing matrix lives in a per-workgroup scratch as hi / lo
+// planes (upper triangle + the lower halves of the 4x4 diagonal tiles), r
+// last.  Panels of PW rows (16; 8 past 512 columns, for the LDS):
+//   A. panel solve: U_k = U_kk^-T A_k, the panel's rows right of its
+//      diagonal block, by forward substitution, one thread per column -> LDS
+//      (an explicit inverse E = U_kk^-T, which parallelises over rows too,
+//      lost 1e3 x strict on an ill-conditioned diagonal block even in
+//      double-double: golden c1_wide sample 6);
+//   B. trailing update A_ij -= sum_p U_pi U_pj over 4x4 tiles (one thread
+//      per tile, products exact by fma, sums carried in double-double), and
+//      -- lookahead -- wave 0 first updates the next panel's diagonal block
+//      (2x2 tiles) and factors it (readlane pivots), while the other seven
+//      waves update the rest.
+// Two barriers per panel (the round-4 kernel: one per pivot, and the whole
+// trailing triangle read and written through scratch at every pivot, ~300 MB
+// per 384-column unit: 77.7 us per unit at B = 1024; profiles/r05a).
+// log d_p summed per pivot; the last pivot is q = r^T N^-1 r - d^T Sigma^-1 d.
 #include "ewarp_dev.h"
 
 namespace ewh_dev {
 namespace {
+
+constexpr int DD_THREADS = 512;
 
 __device__ __forceinline__ dd dd_sub_mul(dd a, dd x, dd y) {   // a - x y
   const double p = x.hi * y.hi;
@@ -33,94 +46,272 @@ __device__ __forceinline__ dd dd_sub_mul(dd a, dd x, dd y) {   // a - x y
   const dd s = dd_two_sum(a.hi, -p);
   return dd_fast(s.hi, s.lo + a.lo - pe);
 }
+// t -= x y, t = (th, tl) carried unnormalised (tl collects the rounding of
+// each step; dd_two_sum(th, tl) at the end)
+__device__ __forceinline__ void dd_acc_sub(double& th, double& tl, dd x, dd y) {
+  const double p = x.hi * y.hi;
+  const double e = fma(x.hi, y.hi, -p) + fma(x.hi, y.lo, x.lo * y.hi);
+  const double s = th - p, bp = s - th;
+  tl += ((th - (s - bp)) + (-p - bp)) - e;
+  th = s;
+}
+// one wave's LDS writes visible to its own later reads (other lanes): the
+// writes complete, and the compiler moves no LDS access across
+__device__ __forceinline__ void lds_wave_sync() { asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory"); }
+__device__ __forceinline__ dd ld2(const double2& v) { return {v.x, v.y}; }
+__device__ __forceinline__ double2 st2(dd v) { return make_double2(v.hi, v.lo); }
+__device__ __forceinline__ dd readlane_dd(dd x, int lane) { return {readlane_d(x.hi, lane), readlane_d(x.lo, lane)}; }
 
-// list != NULL: the units are list[0 .. *count) (absolute unit indices, the
-// verify step's flags); the grid loops over them (a workgroup exits at once
-// when there are none).  list == NULL: units u0 + blockIdx.x.
-__device__ void chol_dd_unit(const CholJob* __restrict__ jobs, int B, long long u, int b_off,
-                             const double* __restrict__ theta, int ldth, double* __restrict__ out_units,
-                             double* __restrict__ scratch, long long scr_per_wg) {
-  __shared__ double rh[WIDE_LD_MAX], rl[WIDE_LD_MAX], wh[WIDE_LD_MAX], wl[WIDE_LD_MAX];
-  __shared__ double red[4];
+// row-major upper triangle of T x T tiles: idx -> (ti, tj)
+__device__ __forceinline__ void tri_decode(int T, int idx, int& ti, int& tj) {
+  const double b = 2.0 * T + 1.0;
+  int i = (int)((b - sqrt(b * b - 8.0 * idx)) * 0.5);
+  auto start = [&](int r) { return r * T - r * (r - 1) / 2; };
+  while (i > 0 && start(i) > idx) --i;
+  while (start(i + 1) <= idx) ++i;
+  ti = i;
+  tj = i + (idx - start(i));
+}
+
+template <int PW>
+struct DdLds {
+  // dynamic LDS: U [PW][n] | DG [PW][PW] | SC [PW] | phinv [n] | red [8]
+  double2 *U, *DG, *SC, *ph;
+  double* red;
+  __device__ DdLds(double2* base, int n) {
+    U = base;
+    DG = U + PW * n;
+    SC = DG + PW * PW;
+    ph = SC + PW;
+    red = (double*)(ph + n);
+  }
+};
+
+template <int PW>
+size_t dd_lds(int n) { return (size_t)(PW * n + PW * PW + PW + n) * sizeof(double2) + 8 * sizeof(double); }
+
+// Wave 0, lanes c < PW: factor the diagonal block DG (upper part valid) of
+// the panel starting at r0; pivots r0 + p < n - 1 add log d_p to ldet and
+// must be positive; the pivot n - 1 is q.  Leaves the strict upper part of
+// U_kk in DG and the scales 1/sqrt(d_p) in SC for the panel solve.
+template <int PW>
+__device__ __forceinline__ void dd_factor_diag(const DdLds<PW>& S, int r0, int n, int lane, double& ldet, bool& ok, double& qv) {
+  dd a[PW];
+#pragma unroll
+  for (int r = 0; r < PW; ++r) a[r] = (lane < PW && r <= lane) ? ld2(S.DG[r * PW + lane]) : dd{0.0, 0.0};
+#pragma unroll
+  for (int p = 0; p < PW; ++p) {
+    const dd d = readlane_dd(a[p], p);
+    if (r0 + p == n - 1) {
+      qv = d.hi + d.lo;
+      if (lane == 0) S.SC[p] = st2({1.0, 0.0});
+      continue;
+    }
+    ok = ok && d.hi > 0.0;
+    ldet += log(d.hi) + d.lo / d.hi;
+    const dd s = dd_div({1.0, 0.0}, dd_sqrt(d));
+    if (lane == 0) S.SC[p] = st2(s);
+    if (lane > p) a[p] = dd_mul(a[p], s);           // U[p][c], c > p
+#pragma unroll
+    for (int r = p + 1; r < PW; ++r) {
+      const dd ur = readlane_dd(a[p], r);
+      if (lane >= r) a[r] = dd_sub_mul(a[r], ur, a[p]);
+    }
+  }
+  // publish U_kk (strict upper part) for the panel solve
+#pragma unroll
+  for (int p = 0; p < PW; ++p)
+    if (lane > p && lane < PW) S.DG[p * PW + lane] = st2(a[p]);
+  lds_wave_sync();
+}
+
+template <int PW>
+__device__ __forceinline__ void chol_ddb_unit(const CholJob* __restrict__ jobs, int B, long long u, int b_off,
+                              const double* __restrict__ theta, double* __restrict__ out_units,
+                              double* __restrict__ scratch, long long scr_per_wg, double2* lds) {
+  // (theta: the unit's own row)
   const int tid = threadIdx.x, wave = tid >> 6, lane = tid & 63;
-  const int p = (int)(u / B), b = (int)(u % B);
-  const CholJob J = jobs[p];
+  // (uniform: the job's fields load into scalar registers, not 50 VGPRs)
+  const int p_ = __builtin_amdgcn_readfirstlane((int)(u / B)), b = __builtin_amdgcn_readfirstlane((int)(u % B));
+  const CholJob& J = jobs[p_];
   const int n = J.ld;
-  const double* Ahi = J.mats + (long long)(b - b_off) * J.mstride;
-  const double* Alo = J.mats_lo ? J.mats_lo + (long long)(b - b_off) * J.mstride : nullptr;
+  const DdLds<PW> S(lds, n);
+  const long long moff = (long long)(b - b_off) * J.mstride;
+  const double* Shi = J.mats + moff;
+  const double* Slo = J.mats_lo ? J.mats_lo + moff : nullptr;
   double* H = scratch + (long long)blockIdx.x * scr_per_wg;
   double* L = H + (long long)n * n;
-  const double* th = theta + (long long)b * ldth;
-  for (int i = wave; i < n; i += 4)
-    for (int j = i + lane; j < n; j += 64) {
-      const long long o = (long long)i * n + j;
-      H[o] = Ahi[o];
-      L[o] = Alo ? Alo[o] : 0.0;
-    }
-  __syncthreads();
+  // phi^-1 per column in double-double (pads and r carry no entry: 0)
   double lphi = 0.0;
-  for (int a = tid; a < J.mreal; a += 256) {
-    if (J.col_ptr[a] == J.col_ptr[a + 1]) continue;          // (pads carry no entry)
-    double ph = 0.0;
-    for (int e = J.col_ptr[a]; e < J.col_ptr[a + 1]; ++e) ph += spec_phi_body(J.spec[e], th);
-    const dd pinv = dd_div({1.0, 0.0}, {ph, 0.0});
-    const long long o = (long long)a * n + a;
-    const dd v = dd_add({H[o], L[o]}, pinv);
-    H[o] = v.hi;
-    L[o] = v.lo;
-    lphi += log(ph);
+  for (int a = tid; a < n; a += DD_THREADS) {
+    dd pinv = {0.0, 0.0};
+    if (a < J.mreal && J.col_ptr[a] < J.col_ptr[a + 1]) {
+      double ph = 0.0;
+      for (int e = J.col_ptr[a]; e < J.col_ptr[a + 1]; ++e) ph += spec_phi_body(J.spec[e], theta);
+      pinv = dd_div({1.0, 0.0}, {ph, 0.0});
+      lphi += log(ph);
+    }
+    S.ph[a] = st2(pinv);
   }
-  lphi = block_sum256(lphi, red);          // (its barriers also publish the diagonal)
-  double ldet = 0.0;
+  lphi = wave_sum(lphi);
+  if (lane == 0) S.red[wave] = lphi;
+  __syncthreads();
+  lphi = 0.0;
+#pragma unroll
+  for (int w = 0; w < DD_THREADS / 64; ++w) lphi += S.red[w];
+  // element (i, j) of the matrix before panel k = 0: S + phi^-1 on the diagonal
+  auto src0 = [&](int i, int j) -> dd {
+    const long long o = (long long)i * n + j;
+    dd v = {Shi[o], Slo ? Slo[o] : 0.0};
+    if (i == j) v = dd_add(v, ld2(S.ph[i]));
+    return v;
+  };
+  double ldet = 0.0, qv = 0.0;
   bool ok = true;
-  for (int k = 0; k < n - 1; ++k) {
-    const long long ok_ = (long long)k * n + k;
-    const dd d = {H[ok_], L[ok_]};
-    ok = ok && (d.hi > 0.0);
-    ldet += log(d.hi) + d.lo / d.hi;
-    for (int j = k + 1 + tid; j < n; j += 256) {
-      const dd r = {H[(long long)k * n + j], L[(long long)k * n + j]};
-      const dd wv = dd_div(r, d);
-      rh[j] = r.hi;
-      rl[j] = r.lo;
-      wh[j] = wv.hi;
-      wl[j] = wv.lo;
+  // panel 0's diagonal block
+  if (wave == 0) {
+    for (int e = lane; e < PW * PW; e += 64) {
+      const int r = e / PW, c = e % PW;
+      if (c >= r) S.DG[e] = st2(src0(r, c));
+    }
+    lds_wave_sync();
+    dd_factor_diag<PW>(S, 0, n, lane, ldet, ok, qv);
+  }
+  __syncthreads();
+  for (int r0 = 0; r0 + PW < n; r0 += PW) {
+    const bool first = r0 == 0;
+    const int t0 = r0 + PW, m = n - t0;
+    // A. panel solve by forward substitution, one thread per column j:
+    // U[p][j] = s_p (A[r0 + p][j] - sum_{r < p} U_kk[r][p] U[r][j])
+    for (int jj = tid; jj < m; jj += DD_THREADS) {
+      const int j = t0 + jj;
+      dd a[PW];
+#pragma unroll
+      for (int r = 0; r < PW; ++r) {
+        const long long o = (long long)(r0 + r) * n + j;
+        a[r] = first ? dd{Shi[o], Slo ? Slo[o] : 0.0} : dd{H[o], L[o]};
+      }
+#pragma unroll
+      for (int p = 0; p < PW; ++p) {
+        double hh = a[p].hi, ll = a[p].lo;
+#pragma unroll
+        for (int r = 0; r < p; ++r) dd_acc_sub(hh, ll, ld2(S.DG[r * PW + p]), a[r]);
+        a[p] = dd_mul(dd_two_sum(hh, ll), ld2(S.SC[p]));
+        S.U[p * n + j] = st2(a[p]);
+      }
     }
     __syncthreads();
-    for (int i = k + 1 + wave; i < n; i += 4) {
-      const dd ri = {rh[i], rl[i]};
-      for (int j = i + lane; j < n; j += 64) {
-        const long long o = (long long)i * n + j;
-        const dd v = dd_sub_mul({H[o], L[o]}, ri, {wh[j], wl[j]});
-        H[o] = v.hi;
-        L[o] = v.lo;
+    // B. trailing update of [t0, n)^2; wave 0: the next diagonal block first
+    const int T = m / 4;
+    if (wave == 0) {
+      constexpr int Q = PW / 2;                  // 2x2 tiles of the PW x PW block
+      for (int e = lane; e < Q * (Q + 1) / 2; e += 64) {
+        int qi, qj;
+        tri_decode(Q, e, qi, qj);
+        const int i0 = t0 + 2 * qi, j0 = t0 + 2 * qj;
+        double ah[2][2], al[2][2];
+#pragma unroll
+        for (int x = 0; x < 2; ++x)
+#pragma unroll
+          for (int y = 0; y < 2; ++y) {
+            const dd v = first ? src0(i0 + x, j0 + y) : dd{H[(long long)(i0 + x) * n + j0 + y], L[(long long)(i0 + x) * n + j0 + y]};
+            ah[x][y] = v.hi;
+            al[x][y] = v.lo;
+          }
+#pragma unroll 1
+        for (int p = 0; p < PW; ++p) {
+          const dd ui[2] = {ld2(S.U[p * n + i0]), ld2(S.U[p * n + i0 + 1])};
+          const dd uj[2] = {ld2(S.U[p * n + j0]), ld2(S.U[p * n + j0 + 1])};
+#pragma unroll
+          for (int x = 0; x < 2; ++x)
+#pragma unroll
+            for (int y = 0; y < 2; ++y) dd_acc_sub(ah[x][y], al[x][y], ui[x], uj[y]);
+        }
+#pragma unroll
+        for (int x = 0; x < 2; ++x)
+#pragma unroll
+          for (int y = 0; y < 2; ++y) {
+            const int r = 2 * qi + x, c = 2 * qj + y;
+            if (c >= r) S.DG[r * PW + c] = st2(dd_two_sum(ah[x][y], al[x][y]));
+          }
+      }
+      lds_wave_sync();
+      dd_factor_diag<PW>(S, t0, n, lane, ldet, ok, qv);
+    } else {
+      constexpr int QD = PW / 4;                 // 4x4 tiles inside the next diagonal block
+      const int ntiles = T * (T + 1) / 2;
+      for (int idx = tid - 64; idx < ntiles; idx += DD_THREADS - 64) {
+        int ti, tj;
+        tri_decode(T, idx, ti, tj);
+        if (tj < QD) continue;                   // (wave 0's)
+        const int i0 = t0 + 4 * ti, j0 = t0 + 4 * tj;
+        double ah[4][4], al[4][4];
+#pragma unroll
+        for (int x = 0; x < 4; ++x)
+#pragma unroll
+          for (int y = 0; y < 4; ++y) {
+            const long long o = (long long)(i0 + x) * n + j0 + y;
+            if (first) {
+              const dd v = src0(i0 + x, j0 + y);
+              ah[x][y] = v.hi;
+              al[x][y] = v.lo;
+            } else {
+              ah[x][y] = H[o];
+              al[x][y] = L[o];
+            }
+          }
+#pragma unroll 1
+        for (int p = 0; p < PW; ++p) {
+          dd ui[4], uj[4];
+#pragma unroll
+          for (int x = 0; x < 4; ++x) {
+            ui[x] = ld2(S.U[p * n + i0 + x]);
+            uj[x] = ld2(S.U[p * n + j0 + x]);
+          }
+#pragma unroll
+          for (int x = 0; x < 4; ++x)
+#pragma unroll
+            for (int y = 0; y < 4; ++y) dd_acc_sub(ah[x][y], al[x][y], ui[x], uj[y]);
+        }
+#pragma unroll
+        for (int x = 0; x < 4; ++x)
+#pragma unroll
+          for (int y = 0; y < 4; ++y) {
+            const long long o = (long long)(i0 + x) * n + j0 + y;
+            const dd v = dd_two_sum(ah[x][y], al[x][y]);
+            H[o] = v.hi;
+            L[o] = v.lo;
+          }
       }
     }
     __threadfence_block();
     __syncthreads();
   }
   if (tid == 0) {
-    const long long o = (long long)(n - 1) * n + (n - 1);
-    const double qv = H[o] + L[o];
     double lnl = J.K[(long long)(b - b_off) * J.kstride] - 0.5 * qv - 0.5 * ldet - 0.5 * lphi;
     if (!ok || J.fail) lnl = -INFINITY;
-    out_units[(long long)p * B + b] = lnl;
+    out_units[(long long)p_ * B + b] = lnl;
   }
   __syncthreads();                         // (the workgroup's next unit reuses LDS and scratch)
 }
 
-__global__ __launch_bounds__(256) void chol_dd_kernel(const CholJob* __restrict__ jobs, int B, long long u0, int b_off,
-                                                      const double* __restrict__ theta, int ldth,
-                                                      double* __restrict__ out_units, double* __restrict__ scratch,
-                                                      long long scr_per_wg, const int* __restrict__ list,
-                                                      const int* __restrict__ count) {
-  if (!list) {
-    chol_dd_unit(jobs, B, u0 + blockIdx.x, b_off, theta, ldth, out_units, scratch, scr_per_wg);
-    return;
+// list != NULL: the units are list[0 .. *count) (absolute unit indices, the
+// verify step's flags); the grid loops over them (a workgroup exits at once
+// when there are none).  list == NULL: units u0 + blockIdx.x.
+template <int PW>
+__global__ __launch_bounds__(DD_THREADS) void chol_dd_kernel(const CholJob* __restrict__ jobs, int B, long long u0,
+                                                             int b_off, const double* __restrict__ theta, int ldth,
+                                                             double* __restrict__ out_units,
+                                                             double* __restrict__ scratch, long long scr_per_wg,
+                                                             const int* __restrict__ list,
+                                                             const int* __restrict__ count) {
+  extern __shared__ __attribute__((aligned(16))) double2 dd_smem[];
+  // one call site (the unit body is inlined once)
+  const int cnt = list ? *count : (int)gridDim.x;
+  for (int i = blockIdx.x; i < cnt; i += gridDim.x) {
+    const long long u = list ? (long long)list[i] : u0 + i;
+    chol_ddb_unit<PW>(jobs, B, u, b_off, theta + (long long)(u % B) * ldth, out_units, scratch, scr_per_wg, dd_smem);
   }
-  const int n = *count;
-  for (int i = blockIdx.x; i < n; i += gridDim.x)
-    chol_dd_unit(jobs, B, list[i], b_off, theta, ldth, out_units, scratch, scr_per_wg);
 }
 
 // The verify step: the forward (a) and reversed (b) fp64 factorisations of
@@ -142,7 +333,38 @@ __global__ __launch_bounds__(256) void verify_units_kernel(const double* __restr
   }
 }
 
+constexpr int DD_PW_WIDE = 8;            // panel rows past DD_LD_PW16 columns (LDS)
+constexpr int DD_LD_PW16 = 512;
+
+template <int PW>
+void launch_dd(const CholJob* jobs, int B, long long u0, int b_off, const double* theta, int ldth, double* units,
+               double* scr, long long scr_per_wg, unsigned grid, const int* list, const int* count, int ld,
+               hipStream_t st) {
+  hipLaunchKernelGGL(HIP_KERNEL_NAME(chol_dd_kernel<PW>), dim3(grid), dim3(DD_THREADS), dd_lds<PW>(ld), st, jobs, B,
+                     u0, b_off, theta, ldth, units, scr, scr_per_wg, list, count);
+}
+
+int launch_dd_any(const CholJob* jobs, int B, long long u0, int b_off, const double* theta, int ldth, double* units,
+                  double* scr, long long scr_per_wg, unsigned grid, const int* list, const int* count, int ld,
+                  hipStream_t st) {
+  if (ld <= DD_LD_PW16)
+    launch_dd<16>(jobs, B, u0, b_off, theta, ldth, units, scr, scr_per_wg, grid, list, count, ld, st);
+  else
+    launch_dd<DD_PW_WIDE>(jobs, B, u0, b_off, theta, ldth, units, scr, scr_per_wg, grid, list, count, ld, st);
+  const hipError_t e = hipGetLastError();
+  return e == hipSuccess ? 0 : set_err(EWH_E_HIP, std::string("chol_dd_kernel: ") + hipGetErrorString(e));
+}
+
 }  // namespace
+
+int set_dd_attributes() {
+  if (hipFuncSetAttribute((const void*)chol_dd_kernel<16>, hipFuncAttributeMaxDynamicSharedMemorySize,
+                          (int)dd_lds<16>(DD_LD_PW16)) != hipSuccess ||
+      hipFuncSetAttribute((const void*)chol_dd_kernel<DD_PW_WIDE>, hipFuncAttributeMaxDynamicSharedMemorySize,
+                          (int)dd_lds<DD_PW_WIDE>(WIDE_LD_MAX)) != hipSuccess)
+    return set_err(EWH_E_HIP, "hipFuncSetAttribute(chol_dd_kernel) failed");
+  return 0;
+}
 
 int launch_verify_units(const double* a, const double* b, long long u0, long long n, int* list, int* count,
                         int* total, hipStream_t st) {
@@ -156,22 +378,19 @@ int launch_verify_units(const double* a, const double* b, long long u0, long lon
 long long dd_scratch_per_wg(int ld) { return 2LL * ld * ld; }
 
 int launch_chol_dd(const CholJob* jobs, int B, long long u0, long long n, int b_off, const double* theta, int ldth,
-                   double* units, double* scr, long long scr_per_wg, long long cap, hipStream_t st) {
-  for (long long o = 0; o < n; o += cap)   // one scratch slot per workgroup of a launch
-    hipLaunchKernelGGL(chol_dd_kernel, dim3((unsigned)std::min(cap, n - o)), dim3(256), 0, st, jobs, B, u0 + o, b_off,
-                       theta, ldth, units, scr, scr_per_wg, nullptr, nullptr);
-  const hipError_t e = hipGetLastError();
-  return e == hipSuccess ? 0 : set_err(EWH_E_HIP, std::string("chol_dd_kernel: ") + hipGetErrorString(e));
+                   double* units, double* scr, long long scr_per_wg, long long cap, int ld, hipStream_t st) {
+  for (long long o = 0; o < n; o += cap) {   // one scratch slot per workgroup of a launch
+    const int rc = launch_dd_any(jobs, B, u0 + o, b_off, theta, ldth, units, scr, scr_per_wg,
+                                 (unsigned)std::min(cap, n - o), nullptr, nullptr, ld, st);
+    if (rc) return rc;
+  }
+  return 0;
 }
 
-
 int launch_chol_dd_list(const CholJob* jobs, int B, int b_off, const double* theta, int ldth, double* units,
-                        double* scr, long long scr_per_wg, long long cap, const int* list, const int* count,
+                        double* scr, long long scr_per_wg, long long cap, const int* list, const int* count, int ld,
                         hipStream_t st) {
-  hipLaunchKernelGGL(chol_dd_kernel, dim3((unsigned)cap), dim3(256), 0, st, jobs, B, 0LL, b_off, theta, ldth, units,
-                     scr, scr_per_wg, list, count);
-  const hipError_t e = hipGetLastError();
-  return e == hipSuccess ? 0 : set_err(EWH_E_HIP, std::string("chol_dd_kernel: ") + hipGetErrorString(e));
+  return launch_dd_any(jobs, B, 0LL, b_off, theta, ldth, units, scr, scr_per_wg, (unsigned)cap, list, count, ld, st);
 }
 
 }  // namespace ewh_dev

@@ -44,6 +44,11 @@ void chol_wide_kernel(const CholJob* __restrict__ jobs, int B, long long u0, int
   const int LD = J.ld, NB = LD >> 4;
   const int nfact = NB - keep;
   const gdptr A = (gdptr)(J.mats + (long long)(b - b_off) * J.mstride);
+  // the reversed (verify) pass reads fl(hi + 2 lo) where the input is held
+  // to double-double (S_lo / G_lo): the forward pass's input is X - lo, this
+  // one's X + lo (to an ulp), so the two straddle the exact input and their
+  // difference also shows how much the input's own rounding moves the lnL
+  const gdptr Alo = (rev && J.mats_lo) ? (gdptr)(J.mats_lo + (long long)(b - b_off) * J.mstride) : nullptr;
   const double* th = theta + (long long)b * ldth;
   __attribute__((address_space(1))) double* scr =
       (__attribute__((address_space(1))) double*)(scratch + (long long)blockIdx.x * scr_per_wg + lane * 4);
@@ -88,7 +93,8 @@ void chol_wide_kernel(const CholJob* __restrict__ jobs, int B, long long u0, int
         if (j < NB) {
           static_for<0, 4>([&](auto RR) {
             constexpr int r = decltype(RR)::value;
-            R[jj][r] = A[(long long)pi(16 * i + q + 4 * r) * LD + pi(16 * j + c)];
+            const long long o = (long long)pi(16 * i + q + 4 * r) * LD + pi(16 * j + c);
+            R[jj][r] = Alo ? A[o] + 2.0 * Alo[o] : A[o];
           });
           if (j == i) {
             const double pd = phinv[pi(16 * i + c)];

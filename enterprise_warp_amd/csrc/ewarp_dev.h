@@ -406,26 +406,74 @@ typedef __attribute__((address_space(1))) void gbl_void_t;
 // ds_bpermute wait (s_waitcnt lgkmcnt(0)) for all matrix loads in flight
 typedef const __attribute__((address_space(1))) double* gdptr;
 
-// block index blk of the upper triangle (row-major over i <= j) -> (i, j)
-constexpr int tri_i(int nb, int blk) {
-  int i = 0;
-  while (blk >= nb - i) { blk -= nb - i; ++i; }
-  return i;
+// Contraction block ownership (contract2_body).  The upper blocks are put in
+// a tiled order -- tiles of th x tw blocks, row-major over the tiles and
+// within one -- and wave v of WS takes a contiguous run of that order (the
+// first NBLK % WS waves one block more).  (th, tw) is picked at compile time
+// to minimise the per-k-step work of the busiest wave: one LDS read per block
+// column it touches and one multiply by the row weight per block row it
+// owns.  Round 4 dealt the blocks round-robin (blk = v + WS sl): C4's 13
+// blocks over 8 waves then read 13 columns and scaled 10 rows per k-step
+// (23 instructions beside 12 MFMAs, and 52 operand registers, which spilled
+// the blocked accumulator); tiled runs: 12 (C2's 9 blocks: 15 -> 8).
+struct CtOrd {
+  int ij[136];                        // i * 64 + j of the pos-th block (NB <= 16)
+};
+constexpr CtOrd ct_order(int nb, int th, int tw) {
+  CtOrd o{};
+  int n = 0;
+  for (int I = 0; I < nb; I += th)
+    for (int J = (I / tw) * tw; J < nb; J += tw)
+      for (int i = I; i < I + th && i < nb; ++i)
+        for (int j = J; j < J + tw && j < nb; ++j)
+          if (j >= i) o.ij[n++] = i * 64 + j;
+  return o;
 }
-constexpr int tri_j(int nb, int blk) {
-  int i = 0;
-  while (blk >= nb - i) { blk -= nb - i; ++i; }
-  return i + blk;
+constexpr int ct_run_start(int nblk, int ws, int v) { return v * (nblk / ws) + (v < nblk % ws ? v : nblk % ws); }
+constexpr int ct_run_len(int nblk, int ws, int v) { return nblk / ws + (v < nblk % ws ? 1 : 0); }
+constexpr int ct_cost(int nb, int ws, int th, int tw) {
+  const CtOrd o = ct_order(nb, th, tw);
+  const int nblk = nb * (nb + 1) / 2;
+  int worst = 0;
+  for (int v = 0; v < ws; ++v) {
+    bool col[16] = {}, row[16] = {};
+    const int s0 = ct_run_start(nblk, ws, v), n = ct_run_len(nblk, ws, v);
+    for (int s = s0; s < s0 + n; ++s) {
+      row[o.ij[s] >> 6] = col[o.ij[s] >> 6] = col[o.ij[s] & 63] = true;
+    }
+    int c = 0;
+    for (int k = 0; k < nb; ++k) c += (col[k] ? 1 : 0) + (row[k] ? 1 : 0);
+    worst = c > worst ? c : worst;
+  }
+  return worst;
 }
-// does wave `wave` of W (blocks wave + W sl) touch block column j as a row (A) / at all?
-constexpr bool wave_uses_row(int nb, int wave, int j, int W = 4) {
-  for (int blk = wave; blk < nb * (nb + 1) / 2; blk += W)
-    if (tri_i(nb, blk) == j) return true;
+constexpr int ct_shape(int nb, int ws) {   // th * 64 + tw
+  int best = 1 << 30, shape = 64 + nb;
+  for (int th = 1; th <= 6; ++th)
+    for (int tw = 1; tw <= nb; ++tw) {
+      const int c = ct_cost(nb, ws, th, tw);
+      if (c < best) {
+        best = c;
+        shape = th * 64 + tw;
+      }
+    }
+  return shape;
+}
+// the (i * 64 + j) of slot sl of wave v under shape SH
+constexpr int ct_blk(int nb, int ws, int sh, int v, int sl) {
+  return ct_order(nb, sh >> 6, sh & 63).ij[ct_run_start(nb * (nb + 1) / 2, ws, v) + sl];
+}
+// does wave v touch block index j as a block row (A operand) / at all?
+constexpr bool ct_uses_row(int nb, int ws, int sh, int v, int j) {
+  for (int sl = 0; sl < ct_run_len(nb * (nb + 1) / 2, ws, v); ++sl)
+    if ((ct_blk(nb, ws, sh, v, sl) >> 6) == j) return true;
   return false;
 }
-constexpr bool wave_uses(int nb, int wave, int j, int W = 4) {
-  for (int blk = wave; blk < nb * (nb + 1) / 2; blk += W)
-    if (tri_i(nb, blk) == j || tri_j(nb, blk) == j) return true;
+constexpr bool ct_uses(int nb, int ws, int sh, int v, int j) {
+  for (int sl = 0; sl < ct_run_len(nb * (nb + 1) / 2, ws, v); ++sl) {
+    const int b = ct_blk(nb, ws, sh, v, sl);
+    if ((b >> 6) == j || (b & 63) == j) return true;
+  }
   return false;
 }
 
@@ -440,7 +488,8 @@ __device__ __forceinline__ void contract2_body(const PsrDev& P, const double* __
   extern __shared__ __attribute__((aligned(16))) double smem[];
   constexpr int LD = 16 * NB;
   constexpr int NBLK = NB * (NB + 1) / 2;
-  constexpr int SLOTS = (NBLK - VW + WS - 1) / WS;
+  constexpr int SH = ct_shape(NB, WS);                // block ownership: tiled runs (ct_order)
+  constexpr int SLOTS = ct_run_len(NBLK, WS, VW);
   constexpr int TILE = CT_ROWS * LD;                 // doubles per tile
   constexpr int CHUNKS = TILE * 8 / 1024;            // 1-KiB glds pieces per tile (4 NB), dealt round-robin to the W waves
   static_assert(CHUNKS * 1024 == TILE * 8, "tile must split into pieces of 1 KiB");
@@ -559,12 +608,12 @@ __device__ __forceinline__ void contract2_body(const PsrDev& P, const double* __
         double tv[NB], av[NB];
         static_for<0, NB>([&](auto J) {
           constexpr int j = decltype(J)::value;
-          if constexpr (wave_uses(NB, VW, j, WS)) tv[j] = trow[16 * j];
-          if constexpr (wave_uses_row(NB, VW, j, WS)) av[j] = wr * tv[j];
+          if constexpr (ct_uses(NB, WS, SH, VW, j)) tv[j] = trow[16 * j];
+          if constexpr (ct_uses_row(NB, WS, SH, VW, j)) av[j] = wr * tv[j];
         });
         static_for<0, SLOTS>([&](auto SL) {
-          constexpr int blk = VW + WS * decltype(SL)::value;
-          constexpr int bi = tri_i(NB, blk), bj = tri_j(NB, blk);
+          constexpr int blk = ct_blk(NB, WS, SH, VW, decltype(SL)::value);
+          constexpr int bi = blk >> 6, bj = blk & 63;
           acc[decltype(SL)::value] = __builtin_amdgcn_mfma_f64_16x16x4f64(av[bi], tv[bj], acc[decltype(SL)::value], 0, 0, 0);
         });
       }
@@ -580,16 +629,19 @@ __device__ __forceinline__ void contract2_body(const PsrDev& P, const double* __
         const int* fe = ebase + cur * CT_ROWS;
         const unsigned fm = (unsigned)__builtin_amdgcn_readfirstlane(fmbase[cur]);
         int nf = 0;
+        // (4 rows per trip beside the blocked accumulator's second register
+        // set, which leaves no room for 8)
+        constexpr int ER = COMP == CT_BLOCKED ? 4 : 8;
 #pragma unroll
-        for (int r0 = 0; r0 < CT_ROWS; r0 += 8) {
-          double tc[8], wc[8];
+        for (int r0 = 0; r0 < CT_ROWS; r0 += ER) {
+          double tc[ER], wc[ER];
 #pragma unroll
-          for (int i = 0; i < 8; ++i) {
+          for (int i = 0; i < ER; ++i) {
             tc[i] = tcol[(r0 + i) * LD];
             wc[i] = ew[r0 + i];
           }
 #pragma unroll
-          for (int i = 0; i < 8; ++i) {
+          for (int i = 0; i < ER; ++i) {
             eacc = fma(wc[i], tc[i], eacc);
             if ((fm >> (r0 + i)) & 1u) {
               const int e = __builtin_amdgcn_readfirstlane(fe[nf]);
@@ -617,8 +669,8 @@ __device__ __forceinline__ void contract2_body(const PsrDev& P, const double* __
   // epilogue: C/D layout lane -> (row q + 4r, col c); mirror to the lower half,
   // unit diagonal on pad columns (m .. LD-2) so they factor as identity.
   static_for<0, SLOTS>([&](auto SL) {
-    constexpr int blk = VW + WS * decltype(SL)::value;
-    constexpr int bi = tri_i(NB, blk), bj = tri_j(NB, blk);
+    constexpr int blk = ct_blk(NB, WS, SH, VW, decltype(SL)::value);
+    constexpr int bi = blk >> 6, bj = blk & 63;
 #pragma unroll
     for (int r = 0; r < 4; ++r) {
       const int row = 16 * bi + q + 4 * r, col = 16 * bj + c;
@@ -1436,11 +1488,14 @@ int launch_chol_lat(int nb, const CholJob* jobs, int B, int P, const double* the
 // keep > 0: the partial factorisation, kept blocks to keep_out as
 // chol_mfma_kernel<KEEP> writes them
 long long wide_scratch_per_wg(int nb, int keep);
-// double-double factorisation (chol_dd.hip), one 256-thread workgroup per
-// unit, 2 ld^2 doubles of scratch each (dd_scratch_per_wg)
+// double-double factorisation (chol_dd.hip), one 512-thread workgroup per
+// unit, 2 ld^2 doubles of scratch each (dd_scratch_per_wg); ld = the jobs'
+// width (one width per launch)
 long long dd_scratch_per_wg(int ld);
 int launch_chol_dd(const CholJob* jobs, int B, long long u0, long long n, int b_off, const double* theta, int ldth,
-                   double* units, double* scr, long long scr_per_wg, long long cap, hipStream_t st);
+                   double* units, double* scr, long long scr_per_wg, long long cap, int ld, hipStream_t st);
+// dynamic-LDS limits of chol_dd_kernel on the current device
+int set_dd_attributes();
 // the verify-and-refine form: units a (forward fp64) vs b (reversed fp64) of
 // [u0, u0 + n) -> list / count of the disagreeing ones (count zeroed by the
 // caller; total, if not NULL: total[0] += the count, total[1] += n), then
@@ -1448,7 +1503,7 @@ int launch_chol_dd(const CholJob* jobs, int B, long long u0, long long n, int b_
 int launch_verify_units(const double* a, const double* b, long long u0, long long n, int* list, int* count,
                         int* total, hipStream_t st);
 int launch_chol_dd_list(const CholJob* jobs, int B, int b_off, const double* theta, int ldth, double* units,
-                        double* scr, long long scr_per_wg, long long cap, const int* list, const int* count,
+                        double* scr, long long scr_per_wg, long long cap, const int* list, const int* count, int ld,
                         hipStream_t st);
 // rev = 1 (keep == 0): the reversed column order (the verify step)
 int launch_chol_wide(const CholJob* jobs, int B, long long u0, long long n, int b_off, const double* theta, int ldth,

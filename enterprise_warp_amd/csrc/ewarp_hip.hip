@@ -30,6 +30,7 @@
 #include <atomic>
 #include <chrono>
 #include <map>
+#include <mutex>
 
 namespace ewh_dev {
 
@@ -1318,7 +1319,8 @@ __global__ void reduce_units_kernel(const double* __restrict__ units, int P, int
 // row_hi, ncol, column-list offset, payload offset; the column lists follow
 // the nseg records) scatters its packed rows x columns payload into the
 // full-layout theta [B x np] of this device.  Columns and rows outside the
-// segments are never read by the context's units.
+// segments are never read by the context's units (stage_theta_range sets them
+// to NaN first).
 __global__ __launch_bounds__(256) void expand_theta_kernel(const double* __restrict__ stage,
                                                            const int* __restrict__ seg, int nseg, int np,
                                                            double* __restrict__ theta) {
@@ -1703,7 +1705,7 @@ int launch_dd_path(DevCtx* h, int nb, const CholJob* jobs, int B, long long u0, 
   const long long per = dd_scratch_per_wg(16 * nb);
   if (h->kernel_mode == MODE_DD) {
     h->dd_forced += n;
-    return launch_chol_dd(jobs, B, u0, n, b_off, theta, ldth, units, h->d_ddscr, per, cap, st);
+    return launch_chol_dd(jobs, B, u0, n, b_off, theta, ldth, units, h->d_ddscr, per, cap, 16 * nb, st);
   }
   int rc;
   if (!h->d_ddstat) {
@@ -1719,7 +1721,7 @@ int launch_dd_path(DevCtx* h, int nb, const CholJob* jobs, int B, long long u0, 
   EWH_HIP(hipMemsetAsync(h->d_ddlist, 0, sizeof(int), st));
   if ((rc = launch_verify_units(units, h->d_units2, u0, n, h->d_ddlist + 1, h->d_ddlist, h->d_ddstat, st))) return rc;
   return launch_chol_dd_list(jobs, B, b_off, theta, ldth, units, h->d_ddscr, per, std::min<long long>(cap, n),
-                             h->d_ddlist + 1, h->d_ddlist, st);
+                             h->d_ddlist + 1, h->d_ddlist, 16 * nb, st);
 }
 
 // the partial factorisation (correlated common process) of units [u0, u0 + n)
@@ -2396,7 +2398,7 @@ int create_ctx(const ewh_pta_desc* d, const std::vector<ProjCoef>& proj, int dev
   if (hipFuncSetAttribute((const void*)chol_lds_kernel, hipFuncAttributeMaxDynamicSharedMemorySize,
                           (int)(LDS_MAX - 64)) != hipSuccess)
     return bail(set_err(EWH_E_HIP, "hipFuncSetAttribute(chol_lds_kernel) failed"));
-  if ((rc = set_contract_attributes())) return bail(rc);
+  if ((rc = set_contract_attributes()) || (rc = set_dd_attributes())) return bail(rc);
   bool any_theta_white = false;
   for (int p = 0; p < h->P; ++p) {
     const ewh_pulsar_desc& s = d->pulsars[p];
@@ -2793,9 +2795,49 @@ struct ewh_handle {
   // contexts with peer access to the first one
   long long h2d_bytes = 0;
   long long peer_mask = 1;
+  // peer-access directions (from, to) this handle holds a reference on
+  // (peer_acquire); released in ewh_destroy
+  std::vector<std::pair<int, int>> peer_held;
 };
 
 namespace {
+
+// Peer access is process-global state.  Handles share it by reference count:
+// a direction (from, to) a handle enabled, or found enabled by another
+// handle, is counted; the last handle to release it disables it.  A direction
+// that was already on when no handle held it (the caller's own) is never
+// counted, so never turned off here.
+std::mutex g_peer_mu;
+std::map<std::pair<int, int>, int> g_peer_refs;
+
+bool peer_acquire(ewh_handle* H, int from, int to) {
+  std::lock_guard<std::mutex> lk(g_peer_mu);
+  if (hipSetDevice(from) != hipSuccess) return false;
+  const hipError_t e = hipDeviceEnablePeerAccess(to, 0);
+  (void)hipGetLastError();
+  const auto key = std::make_pair(from, to);
+  auto it = g_peer_refs.find(key);
+  if (e == hipSuccess || (e == hipErrorPeerAccessAlreadyEnabled && it != g_peer_refs.end())) {
+    ++g_peer_refs[key];
+    H->peer_held.push_back(key);
+    return true;
+  }
+  return e == hipErrorPeerAccessAlreadyEnabled;   // on outside any handle: usable, not ours
+}
+
+void peer_release_all(ewh_handle* H) {
+  std::lock_guard<std::mutex> lk(g_peer_mu);
+  for (const auto& key : H->peer_held) {
+    auto it = g_peer_refs.find(key);
+    if (it == g_peer_refs.end()) continue;
+    if (--it->second == 0) {
+      g_peer_refs.erase(it);
+      if (hipSetDevice(key.first) == hipSuccess) (void)hipDeviceDisablePeerAccess(key.second);
+      (void)hipGetLastError();
+    }
+  }
+  H->peer_held.clear();
+}
 
 // cached: the latency path's record of which host buffer its device address
 // belongs to -- cleared on reallocation (a new buffer may reuse the address)
@@ -2912,6 +2954,10 @@ long long stage_theta_range(ewh_handle* H, DevCtx* h, const double* theta_host, 
   EWH_HIP(hipMemcpyAsync(h->d_seg, h->h_seg, sizeof(int) * (5 * (size_t)nseg + ncolsum), hipMemcpyHostToDevice,
                          h->stream));
   EWH_HIP(hipMemcpyAsync(h->d_stage, h->h_stage, sizeof(double) * payload, hipMemcpyHostToDevice, h->stream));
+  // every entry the segments do not cover reads as NaN (all bits set): a
+  // column some kernel reads but psr_cols does not list gives a non-finite
+  // phi -- a failed sample, not a stale value from an earlier batch
+  EWH_HIP(hipMemsetAsync(h->d_theta, 0xFF, sizeof(double) * (size_t)B * np, h->stream));
   hipLaunchKernelGGL(expand_theta_kernel, dim3(nseg), dim3(256), 0, h->stream, h->d_stage, h->d_seg, nseg, np,
                      h->d_theta);
   EWH_HIP(hipGetLastError());
@@ -3171,13 +3217,9 @@ int ewh_create(const ewh_pta_desc* d, const int32_t* device_ids, int32_t ndev, e
       int a = 0, b = 0;
       if (hipDeviceCanAccessPeer(&a, ids[i], ids[0]) == hipSuccess && hipDeviceCanAccessPeer(&b, ids[0], ids[i]) ==
                                                                              hipSuccess && a && b) {
-        hipError_t e1 = hipSetDevice(ids[i]);
-        if (e1 == hipSuccess) e1 = hipDeviceEnablePeerAccess(ids[0], 0);
-        hipError_t e2 = hipSetDevice(ids[0]);
-        if (e2 == hipSuccess) e2 = hipDeviceEnablePeerAccess(ids[i], 0);
-        ok = (e1 == hipSuccess || e1 == hipErrorPeerAccessAlreadyEnabled) &&
-             (e2 == hipSuccess || e2 == hipErrorPeerAccessAlreadyEnabled);
-        (void)hipGetLastError();
+        const bool a1 = peer_acquire(H, ids[i], ids[0]);
+        const bool a2 = peer_acquire(H, ids[0], ids[i]);
+        ok = a1 && a2;
       }
     }
     if (ok) H->peer_mask |= 1LL << i;
@@ -3483,6 +3525,7 @@ void ewh_destroy(ewh_handle* H) {
     (void)hipFree(H->d_part);
   }
   for (DevCtx* c : H->ctx) destroy_ctx(c);
+  peer_release_all(H);
   if (H->h_theta) (void)hipHostFree(H->h_theta);
   if (H->h_out) (void)hipHostFree(H->h_out);
   delete H;

@@ -257,7 +257,10 @@ double ewh_unit_cost(const ewh_handle* h, int32_t pulsar);
  * bit i set when context i > 0 has peer access to the first context's device
  * (enabled in ewh_create where the devices allow it; the partial B-vectors
  * and gathered blocks then move device to device) -- context 0 and contexts
- * on the first device set their bit too.  Either pointer may be NULL. */
+ * on the first device set their bit too.  Either pointer may be NULL.
+ * Peer access is process-global: handles hold it by reference count, and
+ * ewh_destroy of the last handle holding a direction disables it again (a
+ * direction that was on before any handle enabled it is left on). */
 int ewh_transfer_stats(const ewh_handle* h, int64_t* h2d_bytes, int64_t* peer);
 
 /* The double-double route since the last query (bases past the register
