@@ -24,5 +24,7 @@ fi
 has smoke && step smoke 200 python -c "import __graft_entry__ as g; g.smoke()"
 has bench && step bench 700 python bench.py --steps 20 --warmup 3
 has launch2 && step launch2 300 python bench.py --gpus 2 --dist-backend gloo --same-device --verify --steps 5 --warmup 2 --no-cpu-baseline --no-latency --no-secondary
+has benchsec && step benchsec 500 python bench.py --steps 20 --warmup 3 --no-cpu-baseline --no-latency --no-c5 --no-wide
+has wideonly && step wideonly 400 python bench.py --only-wide
 has wideprof && step wideprof 400 rocprofv3 --kernel-trace --stats -d gpurun_out/profwide_$TAG -o run --output-format csv -- python bench.py --only-wide
 echo ROUND_DONE
