@@ -5,6 +5,7 @@
 //   chol_partial.hip  chol_mfma_kernel<..., KEEP> (correlated common process)
 //   chol_big.hip      chol_big_kernel<NB 10..16>
 //   contract.hip      contract_mfma_kernel / contract2_kernel
+//   contract_wide.hip contract_xr_kernel / contract_wide_kernel (bases past 16 blocks)
 // See ewarp_hip.hip for the formulation.
 #pragma once
 #include <hip/hip_runtime.h>
@@ -1514,6 +1515,9 @@ int launch_partial_nb(int nb, int keep, const CholJob* jobs, int B, long long u0
                       const double* theta, int ldth, double* units, double* keep_out, int keep_bs, hipStream_t st);
 // dynamic-LDS attributes of the contraction kernels on the current device
 int set_contract_attributes();
+// the contraction of a basis past 16 blocks (contract_wide.hip)
+int launch_contract_wide(int nb, const PsrDev& P, const double* w, const double* beta, const double* s,
+                         const double* fac, double* G, int nb_samples, hipStream_t st, double* Glo);
 // true when kernel A/B mode `mode` (>= 3, not 7) is compiled into this library
 // (dev library only: make dev, -DEWH_DEV)
 bool variant_built(int mode);

@@ -1806,13 +1806,18 @@ int ensure_var_scratch(DevCtx* h, int B) {
     maxld = std::max(maxld, (size_t)ps.ld);
     maxfac = std::max(maxfac, (size_t)ps.n_toa * ps.dev.n_bgroup);
   }
-  // chunk: keep G (ld^2) and s (E*ld) scratch under ~1.5 GB
+  // chunk: keep G (ld^2) and s (E*ld) scratch under ~1.5 GB (8 GB for wide bases)
   // epoch-sum rows per sample: whole CT_ROWS tiles (+1) so the pipelined
   // contraction's last epoch tile reads zero-initialised pad rows
   const size_t sstride = ((maxe + CT_ROWS - 1) / CT_ROWS + 1) * CT_ROWS * maxld;
   const bool wide = maxld > 16 * BIG_NB_MAX;        // G_lo for the double-double factorisation
   const size_t per = ((wide ? 2 : 1) * maxld * maxld + sstride + maxn + maxe + maxfac + 1) * sizeof(double);
-  size_t cap = std::min<size_t>(1024, std::max<size_t>(1, (size_t)1536 * 1024 * 1024 / per));
+  // (bases past 16 blocks: 8 GB of the 288 GB HBM, so a batch of up to 1024
+  // samples is one chunk -- one GEMM-form contraction over all of it and one
+  // factorisation launch with 4 units per CU instead of 4 launches of 256
+  // one-wave units)
+  const size_t budget = (wide ? (size_t)8192 : (size_t)1536) * 1024 * 1024;
+  size_t cap = std::min<size_t>(1024, std::max<size_t>(1, budget / per));
   // whole rounds of workgroups over the 256 CUs (a chunk of 853 samples of
   // C2 ran 2 rounds of 512 workgroups, the second two-thirds empty)
   if (cap > 256) cap -= cap % 256;
