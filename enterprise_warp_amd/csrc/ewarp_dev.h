@@ -1509,7 +1509,8 @@ int launch_chol_dd_list(const CholJob* jobs, int B, int b_off, const double* the
 // rev = 1 (keep == 0): the reversed column order (the verify step)
 int launch_chol_wide(const CholJob* jobs, int B, long long u0, long long n, int b_off, const double* theta, int ldth,
                      double* units, double* scr, long long scr_per_wg, long long cap, int keep, double* keep_out,
-                     int keep_b0, int keep_bs, hipStream_t st, int rev = 0);
+                     int keep_b0, int keep_bs, hipStream_t st, int rev = 0, double* units_rev = nullptr,
+                     bool pair = true);
 // keep_out: pulsar-major kept blocks, keep_bs samples per pulsar (see chol_mfma_kernel KEEP)
 int launch_partial_nb(int nb, int keep, const CholJob* jobs, int B, long long u0, long long n, int b_off,
                       const double* theta, int ldth, double* units, double* keep_out, int keep_bs, hipStream_t st);

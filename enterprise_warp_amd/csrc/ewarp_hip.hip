@@ -1387,6 +1387,7 @@ struct PsrHost {
 
 struct DevCtx {
   int device = 0;
+  int n_cu = 256;              // compute units (hipDeviceAttributeMultiprocessorCount)
   int P = 0, n_param = 0;
   bool white_fixed = false;
   int kernel_mode = 0;
@@ -1638,9 +1639,18 @@ bool dd_path(const DevCtx* h, int nb, bool fixed) {
   return nb > BIG_NB_MAX || (fixed && nb > MFMA_NB_MAX);
 }
 
+// Scratch budgets of the wide / double-double factorisations: one slot per
+// resident workgroup.  Round 5 sized them to fill the chip -- 4 GB of the
+// 288 GB HBM: chol_dd_kernel at 384 columns (2.4 MB per workgroup) had run on
+// 56 workgroups (56 of 256 CUs) under the earlier 128 MB, chol_wide_kernel at
+// 24 blocks (600 KB) on 218 waves per launch.  Dev mode 34 keeps the 128 MB
+// budgets and the separate forward / reversed launches (A/B).
+constexpr int MODE_WIDE_R05A = 34;
+long long scratch_budget(const DevCtx* h) { return h->kernel_mode == MODE_WIDE_R05A ? (1LL << 27) : (1LL << 32); }
+
 long long ensure_dd_scratch(DevCtx* h, int ld) {
   const long long per = dd_scratch_per_wg(ld);
-  const long long want = std::min<long long>(1024, std::max<long long>(1, (1LL << 27) / per)) * per;
+  const long long want = std::min<long long>(1024, std::max<long long>(1, scratch_budget(h) / per)) * per;
   if (h->ddscr_len < want) {
     if (h->d_ddscr) {
       (void)hipFree(h->d_ddscr);
@@ -1651,14 +1661,14 @@ long long ensure_dd_scratch(DevCtx* h, int ld) {
     if (dalloc(h, &h->d_ddscr, (size_t)want)) return 0;
     h->ddscr_len = want;
   }
-  return std::min<long long>(1024, h->ddscr_len / per);
+  return std::min<long long>(1024, std::min(h->ddscr_len, want) / per);
 }
 
 // scratch of chol_wide_kernel for (nb, keep): workgroups per launch it holds
-// (0: allocation failed); at most 2048 workgroups, ~1 GB
+// (0: allocation failed); at most 4096 workgroups, <= 4 GB
 long long ensure_wide_scratch(DevCtx* h, int nb, int keep) {
   const long long per = wide_scratch_per_wg(nb, keep);
-  const long long want = std::min<long long>(2048, std::max<long long>(1, (1LL << 27) / per)) * per;
+  const long long want = std::min<long long>(4096, std::max<long long>(1, scratch_budget(h) / per)) * per;
   if (h->widescr_len < want) {
     if (h->d_widescr) {
       (void)hipFree(h->d_widescr);
@@ -1669,16 +1679,17 @@ long long ensure_wide_scratch(DevCtx* h, int nb, int keep) {
     if (dalloc(h, &h->d_widescr, (size_t)want)) return 0;
     h->widescr_len = want;
   }
-  return std::min<long long>(2048, h->widescr_len / per);
+  return std::min<long long>(4096, std::min(h->widescr_len, want) / per);
 }
 
 int launch_wide(DevCtx* h, int nb, int keep, const CholJob* jobs, int B, long long u0, long long n, int b_off,
-                const double* theta, int ldth, double* units, double* keep_out, hipStream_t st, int rev = 0) {
+                const double* theta, int ldth, double* units, double* keep_out, hipStream_t st, int rev = 0,
+                double* units_rev = nullptr) {
   if (nb > WIDE_NB_MAX) return set_err(EWH_E_UNSUPPORTED, "basis wider than 1023 columns");
   const long long cap = ensure_wide_scratch(h, nb, keep);
-  if (cap <= 0) return EWH_E_NOMEM;
+  if (cap <= 0 || (units_rev && cap < 2)) return EWH_E_NOMEM;
   return launch_chol_wide(jobs, B, u0, n, b_off, theta, ldth, units, h->d_widescr, wide_scratch_per_wg(nb, keep), cap,
-                          keep, keep_out, 0, B, st, rev);
+                          keep, keep_out, 0, B, st, rev, units_rev, h->kernel_mode != MODE_WIDE_R05A);
 }
 
 template <typename T>
@@ -1715,9 +1726,20 @@ int launch_dd_path(DevCtx* h, int nb, const CholJob* jobs, int B, long long u0, 
   const size_t U = (size_t)(h->P + (h->corr ? 1 : 0)) * B;
   if ((rc = ensure_buf(h, &h->d_units2, &h->units2_cap, U)) || (rc = ensure_buf(h, &h->d_ddlist, &h->ddlist_cap, U + 1)))
     return rc;
-  if ((rc = launch_wide(h, nb, 0, jobs, B, u0, n, b_off, theta, ldth, units, nullptr, st, 0)) ||
-      (rc = launch_wide(h, nb, 0, jobs, B, u0, n, b_off, theta, ldth, h->d_units2, nullptr, st, 1)))
+  // the forward and reversed fp64 passes: one launch (both in one grid) when
+  // one pass alone would leave SIMD slots empty (chol_wide_kernel: two waves
+  // per SIMD), else two -- past that point the doubled set of resident
+  // scratch slots only adds memory traffic (measured, profiles/r05h: w372
+  // near 2.91 -> 2.40 ms fused at 1024 units; the system model at 4096 units
+  // 1.46 -> 1.75 ms fused); dev mode 34: always two (the round-5a form)
+  const bool fuse = h->kernel_mode != MODE_WIDE_R05A && 2 * n <= 8LL * h->n_cu;
+  if (!fuse) {
+    if ((rc = launch_wide(h, nb, 0, jobs, B, u0, n, b_off, theta, ldth, units, nullptr, st, 0)) ||
+        (rc = launch_wide(h, nb, 0, jobs, B, u0, n, b_off, theta, ldth, h->d_units2, nullptr, st, 1)))
+      return rc;
+  } else if ((rc = launch_wide(h, nb, 0, jobs, B, u0, n, b_off, theta, ldth, units, nullptr, st, 0, h->d_units2))) {
     return rc;
+  }
   EWH_HIP(hipMemsetAsync(h->d_ddlist, 0, sizeof(int), st));
   if ((rc = launch_verify_units(units, h->d_units2, u0, n, h->d_ddlist + 1, h->d_ddlist, h->d_ddstat, st))) return rc;
   return launch_chol_dd_list(jobs, B, b_off, theta, ldth, units, h->d_ddscr, per, std::min<long long>(cap, n),
@@ -2399,6 +2421,8 @@ int create_ctx(const ewh_pta_desc* d, const std::vector<ProjCoef>& proj, int dev
   };
   if (hipStreamCreateWithFlags(&h->stream, hipStreamNonBlocking) != hipSuccess)
     return bail(set_err(EWH_E_HIP, "hipStreamCreate failed"));
+  if (hipDeviceGetAttribute(&h->n_cu, hipDeviceAttributeMultiprocessorCount, device) != hipSuccess || h->n_cu <= 0)
+    h->n_cu = 256;
   // per device (the attribute is a property of the kernel on the current device)
   if (hipFuncSetAttribute((const void*)chol_lds_kernel, hipFuncAttributeMaxDynamicSharedMemorySize,
                           (int)(LDS_MAX - 64)) != hipSuccess)
@@ -3286,14 +3310,14 @@ int ewh_set_fixed_white(ewh_handle* H, const double* values) {
 }
 
 int ewh_set_kernel_mode(ewh_handle* H, int32_t mode) {
-  if (!H || mode < 0 || mode > 33) return set_err(EWH_E_INVALID, "bad handle / mode");
+  if (!H || mode < 0 || mode > 34) return set_err(EWH_E_INVALID, "bad handle / mode");
 #ifdef EWH_DEV
   constexpr bool dev_lib = true;   // mode 33 (the one-proposal C5 schedule with the diagonal launched apart)
 #else
   constexpr bool dev_lib = false;
 #endif
   if (mode != 0 && mode != 1 && mode != 2 && mode != 7 && mode != MODE_WIDE && mode != MODE_DD && !variant_built(mode) &&
-      !(mode == 33 && dev_lib))
+      !((mode == 33 || mode == MODE_WIDE_R05A) && dev_lib))
     return set_err(EWH_E_UNSUPPORTED, "kernel mode " + std::to_string(mode) +
                                           " is not built into this library (A/B variants: the dev library, make dev)");
   for (DevCtx* h : H->ctx) {

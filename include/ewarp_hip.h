@@ -309,7 +309,10 @@ int ewh_refine_stats(ewh_handle* h, int64_t* checked, int64_t* refined);
  * workgroup, 32 = the C5 two-row pass with each streamed slab loaded at the
  * top of its step, 33 = the C5 one-proposal (right-looking) schedule with
  * each diagonal block factored in a launch of its own instead of inside the
- * previous trailing update.  Other modes return EWH_E_UNSUPPORTED. */
+ * previous trailing update, 34 = the wide / double-double route as in round
+ * 5a (separate forward and reversed fp64 launches, 128 MB scratch budgets
+ * that cap the launches at 56-624 workgroups).  Other modes return
+ * EWH_E_UNSUPPORTED. */
 int ewh_set_kernel_mode(ewh_handle* h, int32_t mode);
 
 /* The largest batch the single-launch latency path serves (LAT_B_MAX; a

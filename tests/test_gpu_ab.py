@@ -84,3 +84,19 @@ def test_c5_one_proposal_diag_fusion_bit_identical(B):
                        capture_output=True, text=True, timeout=600, env=env)
     print(r.stdout[-4000:], r.stderr[-2000:])
     assert r.returncode == 0
+
+
+def test_wide_route_schedule_bit_identical():
+    """chol_wide_kernel's paired block rows, the fused forward / reversed
+    verify launch and the chip-filling scratch budgets against the round-5a
+    schedule (dev mode 34): the same lnL bit for bit on the wide goldens, 64
+    prior draws of the 372-column pulsar (white noise fixed and sampled) and
+    the correlated wide partial factorisation (scripts/wide_variant_check.py)."""
+    lib = os.path.join(ROOT, "enterprise_warp_amd", "libewarp_hip_dev.so")
+    if not os.path.exists(lib):
+        pytest.skip("dev library not built (make -C enterprise_warp_amd/csrc dev)")
+    env = dict(os.environ, EWARP_HIP_LIB=lib)
+    r = subprocess.run([sys.executable, os.path.join(ROOT, "scripts", "wide_variant_check.py")],
+                       capture_output=True, text=True, timeout=600, env=env)
+    print(r.stdout[-4000:], r.stderr[-2000:])
+    assert r.returncode == 0
