@@ -125,7 +125,14 @@ __device__ __forceinline__ void dd_factor_diag(const DdLds<PW>& S, int r0, int n
   lds_wave_sync();
 }
 
-template <int PW>
+// RSOLVE (round 5): the panel solve column-oriented -- as soon as U[p][j] is
+// formed it is subtracted from every later row's running sum -- instead of
+// each row summing the earlier ones: the same dd_acc_sub terms in the same
+// order per row (bit-identical), but 15 - p independent updates after each
+// step instead of one dependent chain of p (the solve is one thread per
+// column, so this chain was the panel's critical path).  RSOLVE = false: the
+// round-5a form (dev mode 34).
+template <int PW, bool RSOLVE>
 __device__ __forceinline__ void chol_ddb_unit(const CholJob* __restrict__ jobs, int B, long long u, int b_off,
                               const double* __restrict__ theta, double* __restrict__ out_units,
                               double* __restrict__ scratch, long long scr_per_wg, double2* lds) {
@@ -191,13 +198,29 @@ __device__ __forceinline__ void chol_ddb_unit(const CholJob* __restrict__ jobs, 
         const long long o = (long long)(r0 + r) * n + j;
         a[r] = first ? dd{Shi[o], Slo ? Slo[o] : 0.0} : dd{H[o], L[o]};
       }
+      if constexpr (RSOLVE) {
+        double hh[PW], ll[PW];
 #pragma unroll
-      for (int p = 0; p < PW; ++p) {
-        double hh = a[p].hi, ll = a[p].lo;
+        for (int r = 0; r < PW; ++r) {
+          hh[r] = a[r].hi;
+          ll[r] = a[r].lo;
+        }
 #pragma unroll
-        for (int r = 0; r < p; ++r) dd_acc_sub(hh, ll, ld2(S.DG[r * PW + p]), a[r]);
-        a[p] = dd_mul(dd_two_sum(hh, ll), ld2(S.SC[p]));
-        S.U[p * n + j] = st2(a[p]);
+        for (int p = 0; p < PW; ++p) {
+          const dd up = dd_mul(dd_two_sum(hh[p], ll[p]), ld2(S.SC[p]));
+          S.U[p * n + j] = st2(up);
+#pragma unroll
+          for (int r = p + 1; r < PW; ++r) dd_acc_sub(hh[r], ll[r], ld2(S.DG[p * PW + r]), up);
+        }
+      } else {
+#pragma unroll
+        for (int p = 0; p < PW; ++p) {
+          double hh = a[p].hi, ll = a[p].lo;
+#pragma unroll
+          for (int r = 0; r < p; ++r) dd_acc_sub(hh, ll, ld2(S.DG[r * PW + p]), a[r]);
+          a[p] = dd_mul(dd_two_sum(hh, ll), ld2(S.SC[p]));
+          S.U[p * n + j] = st2(a[p]);
+        }
       }
     }
     __syncthreads();
@@ -298,7 +321,7 @@ __device__ __forceinline__ void chol_ddb_unit(const CholJob* __restrict__ jobs, 
 // list != NULL: the units are list[0 .. *count) (absolute unit indices, the
 // verify step's flags); the grid loops over them (a workgroup exits at once
 // when there are none).  list == NULL: units u0 + blockIdx.x.
-template <int PW>
+template <int PW, bool RSOLVE = true>
 __global__ __launch_bounds__(DD_THREADS) void chol_dd_kernel(const CholJob* __restrict__ jobs, int B, long long u0,
                                                              int b_off, const double* __restrict__ theta, int ldth,
                                                              double* __restrict__ out_units,
@@ -310,7 +333,8 @@ __global__ __launch_bounds__(DD_THREADS) void chol_dd_kernel(const CholJob* __re
   const int cnt = list ? *count : (int)gridDim.x;
   for (int i = blockIdx.x; i < cnt; i += gridDim.x) {
     const long long u = list ? (long long)list[i] : u0 + i;
-    chol_ddb_unit<PW>(jobs, B, u, b_off, theta + (long long)(u % B) * ldth, out_units, scratch, scr_per_wg, dd_smem);
+    chol_ddb_unit<PW, RSOLVE>(jobs, B, u, b_off, theta + (long long)(u % B) * ldth, out_units, scratch, scr_per_wg,
+                              dd_smem);
   }
 }
 
@@ -339,18 +363,22 @@ constexpr int DD_LD_PW16 = 512;
 template <int PW>
 void launch_dd(const CholJob* jobs, int B, long long u0, int b_off, const double* theta, int ldth, double* units,
                double* scr, long long scr_per_wg, unsigned grid, const int* list, const int* count, int ld,
-               hipStream_t st) {
-  hipLaunchKernelGGL(HIP_KERNEL_NAME(chol_dd_kernel<PW>), dim3(grid), dim3(DD_THREADS), dd_lds<PW>(ld), st, jobs, B,
-                     u0, b_off, theta, ldth, units, scr, scr_per_wg, list, count);
+               hipStream_t st, bool r05a) {
+  if (r05a)
+    hipLaunchKernelGGL(HIP_KERNEL_NAME(chol_dd_kernel<PW, false>), dim3(grid), dim3(DD_THREADS), dd_lds<PW>(ld), st,
+                       jobs, B, u0, b_off, theta, ldth, units, scr, scr_per_wg, list, count);
+  else
+    hipLaunchKernelGGL(HIP_KERNEL_NAME(chol_dd_kernel<PW, true>), dim3(grid), dim3(DD_THREADS), dd_lds<PW>(ld), st,
+                       jobs, B, u0, b_off, theta, ldth, units, scr, scr_per_wg, list, count);
 }
 
 int launch_dd_any(const CholJob* jobs, int B, long long u0, int b_off, const double* theta, int ldth, double* units,
                   double* scr, long long scr_per_wg, unsigned grid, const int* list, const int* count, int ld,
-                  hipStream_t st) {
+                  hipStream_t st, bool r05a) {
   if (ld <= DD_LD_PW16)
-    launch_dd<16>(jobs, B, u0, b_off, theta, ldth, units, scr, scr_per_wg, grid, list, count, ld, st);
+    launch_dd<16>(jobs, B, u0, b_off, theta, ldth, units, scr, scr_per_wg, grid, list, count, ld, st, r05a);
   else
-    launch_dd<DD_PW_WIDE>(jobs, B, u0, b_off, theta, ldth, units, scr, scr_per_wg, grid, list, count, ld, st);
+    launch_dd<DD_PW_WIDE>(jobs, B, u0, b_off, theta, ldth, units, scr, scr_per_wg, grid, list, count, ld, st, r05a);
   const hipError_t e = hipGetLastError();
   return e == hipSuccess ? 0 : set_err(EWH_E_HIP, std::string("chol_dd_kernel: ") + hipGetErrorString(e));
 }
@@ -358,9 +386,13 @@ int launch_dd_any(const CholJob* jobs, int B, long long u0, int b_off, const dou
 }  // namespace
 
 int set_dd_attributes() {
-  if (hipFuncSetAttribute((const void*)chol_dd_kernel<16>, hipFuncAttributeMaxDynamicSharedMemorySize,
+  if (hipFuncSetAttribute((const void*)chol_dd_kernel<16, true>, hipFuncAttributeMaxDynamicSharedMemorySize,
                           (int)dd_lds<16>(DD_LD_PW16)) != hipSuccess ||
-      hipFuncSetAttribute((const void*)chol_dd_kernel<DD_PW_WIDE>, hipFuncAttributeMaxDynamicSharedMemorySize,
+      hipFuncSetAttribute((const void*)chol_dd_kernel<DD_PW_WIDE, true>, hipFuncAttributeMaxDynamicSharedMemorySize,
+                          (int)dd_lds<DD_PW_WIDE>(WIDE_LD_MAX)) != hipSuccess ||
+      hipFuncSetAttribute((const void*)chol_dd_kernel<16, false>, hipFuncAttributeMaxDynamicSharedMemorySize,
+                          (int)dd_lds<16>(DD_LD_PW16)) != hipSuccess ||
+      hipFuncSetAttribute((const void*)chol_dd_kernel<DD_PW_WIDE, false>, hipFuncAttributeMaxDynamicSharedMemorySize,
                           (int)dd_lds<DD_PW_WIDE>(WIDE_LD_MAX)) != hipSuccess)
     return set_err(EWH_E_HIP, "hipFuncSetAttribute(chol_dd_kernel) failed");
   return 0;
@@ -378,10 +410,10 @@ int launch_verify_units(const double* a, const double* b, long long u0, long lon
 long long dd_scratch_per_wg(int ld) { return 2LL * ld * ld; }
 
 int launch_chol_dd(const CholJob* jobs, int B, long long u0, long long n, int b_off, const double* theta, int ldth,
-                   double* units, double* scr, long long scr_per_wg, long long cap, int ld, hipStream_t st) {
+                   double* units, double* scr, long long scr_per_wg, long long cap, int ld, hipStream_t st, bool r05a) {
   for (long long o = 0; o < n; o += cap) {   // one scratch slot per workgroup of a launch
     const int rc = launch_dd_any(jobs, B, u0 + o, b_off, theta, ldth, units, scr, scr_per_wg,
-                                 (unsigned)std::min(cap, n - o), nullptr, nullptr, ld, st);
+                                 (unsigned)std::min(cap, n - o), nullptr, nullptr, ld, st, r05a);
     if (rc) return rc;
   }
   return 0;
@@ -389,8 +421,9 @@ int launch_chol_dd(const CholJob* jobs, int B, long long u0, long long n, int b_
 
 int launch_chol_dd_list(const CholJob* jobs, int B, int b_off, const double* theta, int ldth, double* units,
                         double* scr, long long scr_per_wg, long long cap, const int* list, const int* count, int ld,
-                        hipStream_t st) {
-  return launch_dd_any(jobs, B, 0LL, b_off, theta, ldth, units, scr, scr_per_wg, (unsigned)cap, list, count, ld, st);
+                        hipStream_t st, bool r05a) {
+  return launch_dd_any(jobs, B, 0LL, b_off, theta, ldth, units, scr, scr_per_wg, (unsigned)cap, list, count, ld, st,
+                       r05a);
 }
 
 }  // namespace ewh_dev

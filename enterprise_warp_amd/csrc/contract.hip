@@ -43,6 +43,10 @@ constexpr size_t contract2_lds(int nb) { return (size_t)(2 * CT_ROWS * 16 * nb +
 // waves per sample: 4, or 8 where measured faster (fewer accumulators per
 // wave: more waves per SIMD to hide the k-steps' LDS latency)
 constexpr int contract2_default_waves(int nb) { return nb >= 9 ? 8 : 4; }
+// the run remainder on the last waves (ct_run_start) where the accumulator is
+// single (NB <= 9: C2's ECORR model); the blocked NB >= 10 kernel keeps the
+// round-4 order -- with the remainder moved its spill grew 12 -> 28 B/lane
+constexpr bool contract2_late(int nb) { return nb <= 9; }
 
 template <int NB>
 int launch_contract2(int waves, const PsrDev& P, const double* w, const double* beta, double* s, long long s_stride,
@@ -57,14 +61,24 @@ int launch_contract2(int waves, const PsrDev& P, const double* w, const double* 
       return 0;
     }
   }
+  if (waves == 35) {     // (dev A/B: the extra blocks on the first waves, round 4-5a)
+    if (contract2_default_waves(NB) == 8)
+      hipLaunchKernelGGL(HIP_KERNEL_NAME(contract2_kernel<NB, 8, CP, false>), dim3(nb_samples), dim3(512),
+                         contract2_lds(NB), st, P, w, beta, s, s_stride, G);
+    else
+      hipLaunchKernelGGL(HIP_KERNEL_NAME(contract2_kernel<NB, 4, CP, false>), dim3(nb_samples), dim3(256),
+                         contract2_lds(NB), st, P, w, beta, s, s_stride, G);
+    return 0;
+  }
 #endif
   if (waves == 0 || waves == 30) waves = contract2_default_waves(NB);
+  constexpr bool LT = contract2_late(NB);
   if (waves == 8)
-    hipLaunchKernelGGL(HIP_KERNEL_NAME(contract2_kernel<NB, 8, CP>), dim3(nb_samples), dim3(512), contract2_lds(NB),
-                       st, P, w, beta, s, s_stride, G);
+    hipLaunchKernelGGL(HIP_KERNEL_NAME(contract2_kernel<NB, 8, CP, LT>), dim3(nb_samples), dim3(512),
+                       contract2_lds(NB), st, P, w, beta, s, s_stride, G);
   else
-    hipLaunchKernelGGL(HIP_KERNEL_NAME(contract2_kernel<NB, 4, CP>), dim3(nb_samples), dim3(256), contract2_lds(NB),
-                       st, P, w, beta, s, s_stride, G);
+    hipLaunchKernelGGL(HIP_KERNEL_NAME(contract2_kernel<NB, 4, CP, LT>), dim3(nb_samples), dim3(256),
+                       contract2_lds(NB), st, P, w, beta, s, s_stride, G);
   return 0;
 }
 
@@ -81,14 +95,19 @@ int dispatch_contract2(int nb, int waves, const PsrDev& P, const double* w, cons
 template <int NB>
 int set_attr2() {
   constexpr int CP = contract2_comp(NB);
-  EWH_HIP(hipFuncSetAttribute((const void*)contract2_kernel<NB, 4, CP>, hipFuncAttributeMaxDynamicSharedMemorySize,
-                              (int)contract2_lds(NB)));
-  EWH_HIP(hipFuncSetAttribute((const void*)contract2_kernel<NB, 8, CP>, hipFuncAttributeMaxDynamicSharedMemorySize,
-                              (int)contract2_lds(NB)));
+  constexpr bool LT = contract2_late(NB);
+  EWH_HIP(hipFuncSetAttribute((const void*)contract2_kernel<NB, 4, CP, LT>,
+                              hipFuncAttributeMaxDynamicSharedMemorySize, (int)contract2_lds(NB)));
+  EWH_HIP(hipFuncSetAttribute((const void*)contract2_kernel<NB, 8, CP, LT>,
+                              hipFuncAttributeMaxDynamicSharedMemorySize, (int)contract2_lds(NB)));
 #ifdef EWH_DEV
   if constexpr (NB <= 10)
     EWH_HIP(hipFuncSetAttribute((const void*)contract2_kernel<NB, 8, CT_TWOSUM>,
                                 hipFuncAttributeMaxDynamicSharedMemorySize, (int)contract2_lds(NB)));
+  EWH_HIP(hipFuncSetAttribute((const void*)contract2_kernel<NB, 4, CP, false>,
+                              hipFuncAttributeMaxDynamicSharedMemorySize, (int)contract2_lds(NB)));
+  EWH_HIP(hipFuncSetAttribute((const void*)contract2_kernel<NB, 8, CP, false>,
+                              hipFuncAttributeMaxDynamicSharedMemorySize, (int)contract2_lds(NB)));
 #endif
   return 0;
 }

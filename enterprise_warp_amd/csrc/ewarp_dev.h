@@ -430,15 +430,28 @@ constexpr CtOrd ct_order(int nb, int th, int tw) {
           if (j >= i) o.ij[n++] = i * 64 + j;
   return o;
 }
-constexpr int ct_run_start(int nblk, int ws, int v) { return v * (nblk / ws) + (v < nblk % ws ? v : nblk % ws); }
-constexpr int ct_run_len(int nblk, int ws, int v) { return nblk / ws + (v < nblk % ws ? 1 : 0); }
-constexpr int ct_cost(int nb, int ws, int th, int tw) {
+// Runs: wave v of ws takes nblk / ws blocks, and the nblk % ws remainder goes
+// one each to the LAST waves (LATE, round 5): waves 0 .. ceil(LD / 64) - 1
+// also carry the ECORR epoch sums (threads tid < LD) and wave 0 the per-tile
+// weight staging, so they take the shorter runs (round 4: the first waves
+// took the extra blocks -- C2's 45 blocks put 6 MFMA blocks AND the epoch
+// sums on waves 0-2; dev mode 35 keeps that order for the A/B).  Used where
+// the accumulator is single (contract2_late: NB <= 9)
+constexpr int ct_run_start(int nblk, int ws, int v, bool late = true) {
+  const int b = nblk / ws, x = nblk % ws;
+  return late ? v * b + (v > ws - x ? v - (ws - x) : 0) : v * b + (v < x ? v : x);
+}
+constexpr int ct_run_len(int nblk, int ws, int v, bool late = true) {
+  const int b = nblk / ws, x = nblk % ws;
+  return b + ((late ? v >= ws - x : v < x) ? 1 : 0);
+}
+constexpr int ct_cost(int nb, int ws, int th, int tw, bool late = true) {
   const CtOrd o = ct_order(nb, th, tw);
   const int nblk = nb * (nb + 1) / 2;
   int worst = 0;
   for (int v = 0; v < ws; ++v) {
     bool col[16] = {}, row[16] = {};
-    const int s0 = ct_run_start(nblk, ws, v), n = ct_run_len(nblk, ws, v);
+    const int s0 = ct_run_start(nblk, ws, v, late), n = ct_run_len(nblk, ws, v, late);
     for (int s = s0; s < s0 + n; ++s) {
       row[o.ij[s] >> 6] = col[o.ij[s] >> 6] = col[o.ij[s] & 63] = true;
     }
@@ -448,11 +461,11 @@ constexpr int ct_cost(int nb, int ws, int th, int tw) {
   }
   return worst;
 }
-constexpr int ct_shape(int nb, int ws) {   // th * 64 + tw
+constexpr int ct_shape(int nb, int ws, bool late = true) {   // th * 64 + tw
   int best = 1 << 30, shape = 64 + nb;
   for (int th = 1; th <= 6; ++th)
     for (int tw = 1; tw <= nb; ++tw) {
-      const int c = ct_cost(nb, ws, th, tw);
+      const int c = ct_cost(nb, ws, th, tw, late);
       if (c < best) {
         best = c;
         shape = th * 64 + tw;
@@ -461,18 +474,18 @@ constexpr int ct_shape(int nb, int ws) {   // th * 64 + tw
   return shape;
 }
 // the (i * 64 + j) of slot sl of wave v under shape SH
-constexpr int ct_blk(int nb, int ws, int sh, int v, int sl) {
-  return ct_order(nb, sh >> 6, sh & 63).ij[ct_run_start(nb * (nb + 1) / 2, ws, v) + sl];
+constexpr int ct_blk(int nb, int ws, int sh, int v, int sl, bool late = true) {
+  return ct_order(nb, sh >> 6, sh & 63).ij[ct_run_start(nb * (nb + 1) / 2, ws, v, late) + sl];
 }
 // does wave v touch block index j as a block row (A operand) / at all?
-constexpr bool ct_uses_row(int nb, int ws, int sh, int v, int j) {
-  for (int sl = 0; sl < ct_run_len(nb * (nb + 1) / 2, ws, v); ++sl)
-    if ((ct_blk(nb, ws, sh, v, sl) >> 6) == j) return true;
+constexpr bool ct_uses_row(int nb, int ws, int sh, int v, int j, bool late = true) {
+  for (int sl = 0; sl < ct_run_len(nb * (nb + 1) / 2, ws, v, late); ++sl)
+    if ((ct_blk(nb, ws, sh, v, sl, late) >> 6) == j) return true;
   return false;
 }
-constexpr bool ct_uses(int nb, int ws, int sh, int v, int j) {
-  for (int sl = 0; sl < ct_run_len(nb * (nb + 1) / 2, ws, v); ++sl) {
-    const int b = ct_blk(nb, ws, sh, v, sl);
+constexpr bool ct_uses(int nb, int ws, int sh, int v, int j, bool late = true) {
+  for (int sl = 0; sl < ct_run_len(nb * (nb + 1) / 2, ws, v, late); ++sl) {
+    const int b = ct_blk(nb, ws, sh, v, sl, late);
     if ((b >> 6) == j || (b & 63) == j) return true;
   }
   return false;
@@ -482,15 +495,15 @@ constexpr bool ct_uses(int nb, int ws, int sh, int v, int j) {
 // per-tile weights); VW / WS: the virtual wave that picks the output blocks
 // (blocks VW + WS sl) and the virtual waves per sample -- WS = W SPLIT when a
 // sample's blocks are split over SPLIT workgroups (contract2_kernel).
-template <int NB, int WAVE, int W, int VW = WAVE, int WS = W, int COMP = CT_BLOCKED>
+template <int NB, int WAVE, int W, int VW = WAVE, int WS = W, int COMP = CT_BLOCKED, bool LATE = true>
 __device__ __forceinline__ void contract2_body(const PsrDev& P, const double* __restrict__ wrow,
                                                const double* __restrict__ brow, double* __restrict__ srow,
                                                double* __restrict__ Gout) {
   extern __shared__ __attribute__((aligned(16))) double smem[];
   constexpr int LD = 16 * NB;
   constexpr int NBLK = NB * (NB + 1) / 2;
-  constexpr int SH = ct_shape(NB, WS);                // block ownership: tiled runs (ct_order)
-  constexpr int SLOTS = ct_run_len(NBLK, WS, VW);
+  constexpr int SH = ct_shape(NB, WS, LATE);          // block ownership: tiled runs (ct_order)
+  constexpr int SLOTS = ct_run_len(NBLK, WS, VW, LATE);
   constexpr int TILE = CT_ROWS * LD;                 // doubles per tile
   constexpr int CHUNKS = TILE * 8 / 1024;            // 1-KiB glds pieces per tile (4 NB), dealt round-robin to the W waves
   static_assert(CHUNKS * 1024 == TILE * 8, "tile must split into pieces of 1 KiB");
@@ -609,11 +622,11 @@ __device__ __forceinline__ void contract2_body(const PsrDev& P, const double* __
         double tv[NB], av[NB];
         static_for<0, NB>([&](auto J) {
           constexpr int j = decltype(J)::value;
-          if constexpr (ct_uses(NB, WS, SH, VW, j)) tv[j] = trow[16 * j];
-          if constexpr (ct_uses_row(NB, WS, SH, VW, j)) av[j] = wr * tv[j];
+          if constexpr (ct_uses(NB, WS, SH, VW, j, LATE)) tv[j] = trow[16 * j];
+          if constexpr (ct_uses_row(NB, WS, SH, VW, j, LATE)) av[j] = wr * tv[j];
         });
         static_for<0, SLOTS>([&](auto SL) {
-          constexpr int blk = ct_blk(NB, WS, SH, VW, decltype(SL)::value);
+          constexpr int blk = ct_blk(NB, WS, SH, VW, decltype(SL)::value, LATE);
           constexpr int bi = blk >> 6, bj = blk & 63;
           acc[decltype(SL)::value] = __builtin_amdgcn_mfma_f64_16x16x4f64(av[bi], tv[bj], acc[decltype(SL)::value], 0, 0, 0);
         });
@@ -670,7 +683,7 @@ __device__ __forceinline__ void contract2_body(const PsrDev& P, const double* __
   // epilogue: C/D layout lane -> (row q + 4r, col c); mirror to the lower half,
   // unit diagonal on pad columns (m .. LD-2) so they factor as identity.
   static_for<0, SLOTS>([&](auto SL) {
-    constexpr int blk = ct_blk(NB, WS, SH, VW, decltype(SL)::value);
+    constexpr int blk = ct_blk(NB, WS, SH, VW, decltype(SL)::value, LATE);
     constexpr int bi = blk >> 6, bj = blk & 63;
 #pragma unroll
     for (int r = 0; r < 4; ++r) {
@@ -686,7 +699,7 @@ __device__ __forceinline__ void contract2_body(const PsrDev& P, const double* __
 
 // W = 4 or 8 waves per workgroup (8: half the accumulators per wave, so the
 // narrow NB = 9 kernel fits 4 waves per SIMD and the wide NB = 13 one 2).
-template <int NB, int W, int COMP = CT_BLOCKED>
+template <int NB, int W, int COMP = CT_BLOCKED, bool LATE = true>
 __global__ __launch_bounds__(64 * W) void contract2_kernel(PsrDev P, const double* __restrict__ w,
                                                            const double* __restrict__ beta, double* __restrict__ s,
                                                            long long s_stride, double* __restrict__ G) {
@@ -698,7 +711,7 @@ __global__ __launch_bounds__(64 * W) void contract2_kernel(PsrDev P, const doubl
   const int wv = threadIdx.x >> 6;
   static_for<0, W>([&](auto WV) {
     constexpr int wave = decltype(WV)::value;
-    if (wv == wave) contract2_body<NB, wave, W, wave, W, COMP>(P, wrow, brow, srow, Gout);
+    if (wv == wave) contract2_body<NB, wave, W, wave, W, COMP, LATE>(P, wrow, brow, srow, Gout);
   });
 }
 // the accumulation per width: blocked from 10 blocks on (C4's 13: the same
@@ -1494,18 +1507,20 @@ long long wide_scratch_per_wg(int nb, int keep);
 // width (one width per launch)
 long long dd_scratch_per_wg(int ld);
 int launch_chol_dd(const CholJob* jobs, int B, long long u0, long long n, int b_off, const double* theta, int ldth,
-                   double* units, double* scr, long long scr_per_wg, long long cap, int ld, hipStream_t st);
+                   double* units, double* scr, long long scr_per_wg, long long cap, int ld, hipStream_t st,
+                   bool r05a = false);
 // dynamic-LDS limits of chol_dd_kernel on the current device
 int set_dd_attributes();
 // the verify-and-refine form: units a (forward fp64) vs b (reversed fp64) of
 // [u0, u0 + n) -> list / count of the disagreeing ones (count zeroed by the
 // caller; total, if not NULL: total[0] += the count, total[1] += n), then
-// chol_dd_kernel over the list (cap workgroups looping) into units
+// chol_dd_kernel over the list (cap workgroups looping) into units; r05a: the
+// round-5a panel solve (row-oriented; dev mode 34)
 int launch_verify_units(const double* a, const double* b, long long u0, long long n, int* list, int* count,
                         int* total, hipStream_t st);
 int launch_chol_dd_list(const CholJob* jobs, int B, int b_off, const double* theta, int ldth, double* units,
                         double* scr, long long scr_per_wg, long long cap, const int* list, const int* count, int ld,
-                        hipStream_t st);
+                        hipStream_t st, bool r05a = false);
 // rev = 1 (keep == 0): the reversed column order (the verify step)
 int launch_chol_wide(const CholJob* jobs, int B, long long u0, long long n, int b_off, const double* theta, int ldth,
                      double* units, double* scr, long long scr_per_wg, long long cap, int keep, double* keep_out,

@@ -1716,7 +1716,8 @@ int launch_dd_path(DevCtx* h, int nb, const CholJob* jobs, int B, long long u0, 
   const long long per = dd_scratch_per_wg(16 * nb);
   if (h->kernel_mode == MODE_DD) {
     h->dd_forced += n;
-    return launch_chol_dd(jobs, B, u0, n, b_off, theta, ldth, units, h->d_ddscr, per, cap, 16 * nb, st);
+    return launch_chol_dd(jobs, B, u0, n, b_off, theta, ldth, units, h->d_ddscr, per, cap, 16 * nb, st,
+                          h->kernel_mode == MODE_WIDE_R05A);
   }
   int rc;
   if (!h->d_ddstat) {
@@ -1743,7 +1744,7 @@ int launch_dd_path(DevCtx* h, int nb, const CholJob* jobs, int B, long long u0, 
   EWH_HIP(hipMemsetAsync(h->d_ddlist, 0, sizeof(int), st));
   if ((rc = launch_verify_units(units, h->d_units2, u0, n, h->d_ddlist + 1, h->d_ddlist, h->d_ddstat, st))) return rc;
   return launch_chol_dd_list(jobs, B, b_off, theta, ldth, units, h->d_ddscr, per, std::min<long long>(cap, n),
-                             h->d_ddlist + 1, h->d_ddlist, 16 * nb, st);
+                             h->d_ddlist + 1, h->d_ddlist, 16 * nb, st, h->kernel_mode == MODE_WIDE_R05A);
 }
 
 // the partial factorisation (correlated common process) of units [u0, u0 + n)
@@ -1878,7 +1879,9 @@ int run_white(DevCtx* h, int p, const double* theta, int ldth, int b0, int nb) {
   if (ps.dev.n_bgroup == 0 && h->kernel_mode != 7 && ps.nb <= CONTRACT2_NB_MAX) {
     // (dev library A/B: mode 15 = 4 waves per sample, mode 16 = 8)
     // (30: TwoSum accumulation up to 10 blocks)
-    const int waves = h->kernel_mode == 15 ? 4 : h->kernel_mode == 16 ? 8 : h->kernel_mode == 30 ? 30 : 0;
+    // (35: the run remainder on the first waves, as in round 4-5a)
+    const int waves = h->kernel_mode == 15 ? 4 : h->kernel_mode == 16 ? 8 : h->kernel_mode == 30 ? 30
+                    : h->kernel_mode == 35 ? 35 : 0;
     int rc = launch_contract2_nb(ps.nb, waves, ps.dev, h->d_w, h->d_beta, h->d_s, h->s_stride, h->d_G, nb, h->stream);
     if (rc) return rc;
     EWH_HIP(hipGetLastError());
@@ -3310,14 +3313,14 @@ int ewh_set_fixed_white(ewh_handle* H, const double* values) {
 }
 
 int ewh_set_kernel_mode(ewh_handle* H, int32_t mode) {
-  if (!H || mode < 0 || mode > 34) return set_err(EWH_E_INVALID, "bad handle / mode");
+  if (!H || mode < 0 || mode > 35) return set_err(EWH_E_INVALID, "bad handle / mode");
 #ifdef EWH_DEV
   constexpr bool dev_lib = true;   // mode 33 (the one-proposal C5 schedule with the diagonal launched apart)
 #else
   constexpr bool dev_lib = false;
 #endif
   if (mode != 0 && mode != 1 && mode != 2 && mode != 7 && mode != MODE_WIDE && mode != MODE_DD && !variant_built(mode) &&
-      !((mode == 33 || mode == MODE_WIDE_R05A) && dev_lib))
+      !((mode == 33 || mode == MODE_WIDE_R05A || mode == 35) && dev_lib))
     return set_err(EWH_E_UNSUPPORTED, "kernel mode " + std::to_string(mode) +
                                           " is not built into this library (A/B variants: the dev library, make dev)");
   for (DevCtx* h : H->ctx) {

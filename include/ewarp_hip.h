@@ -311,7 +311,9 @@ int ewh_refine_stats(ewh_handle* h, int64_t* checked, int64_t* refined);
  * each diagonal block factored in a launch of its own instead of inside the
  * previous trailing update, 34 = the wide / double-double route as in round
  * 5a (separate forward and reversed fp64 launches, 128 MB scratch budgets
- * that cap the launches at 56-624 workgroups).  Other modes return
+ * that cap the launches at 56-624 workgroups), 35 = the varying-white-noise
+ * contraction with the blocks' remainder on the first waves (round 4-5a:
+ * the waves that also form the ECORR epoch sums).  Other modes return
  * EWH_E_UNSUPPORTED. */
 int ewh_set_kernel_mode(ewh_handle* h, int32_t mode);
 

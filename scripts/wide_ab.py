@@ -1,4 +1,4 @@
-"""Interleaved A/B timing of the wide / double-double route (bases past the
+"""Interleaved A/B timing of kernel modes -- written for the wide / double-double route (bases past the
 register kernels: the 372-column 10k-TOA pulsar with white noise fixed and
 sampled, and the reference's system_noise_example model) between kernel
 modes, on prior and near-truth draws; per mode the median ms per batch, the
@@ -6,6 +6,7 @@ refined share (ewh_refine_stats) and the largest difference from the first
 mode in strict units (modes that only change launch shapes must be 0).
 
     python scripts/wide_ab.py [--cases w372_fixed,system] [--modes 0,34,27,29] [--rounds 5]
+    python scripts/wide_ab.py --cases c2,c4 --modes 0,35 --kinds prior --contract
 
 Loads the dev library (mode 34 and the other A/B modes live there only)
 unless EWARP_HIP_LIB names another build.
@@ -30,6 +31,8 @@ def make_case(name):
         return synth.config_wide(False)
     if name == "system":
         return synth.config_system(os.path.join(ROOT, "tests", "golden", "ref_examples"))
+    if name in ("c2", "c3", "c4"):
+        return getattr(synth, f"config_{name}")()
     raise SystemExit(f"unknown case {name}")
 
 
@@ -39,6 +42,8 @@ def main():
     ap.add_argument("--modes", default="0,34")
     ap.add_argument("--rounds", type=int, default=5)
     ap.add_argument("--kinds", default="prior,near")
+    ap.add_argument("--contract", action="store_true",
+                    help="time the contraction stage alone (ewh_contract_device) instead of the lnL batch")
     args = ap.parse_args()
     import torch
     from enterprise_warp_amd import synth
@@ -63,9 +68,15 @@ def main():
                     s, e = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
                     torch.cuda.synchronize()
                     s.record()
-                    eng.lnl_units_device(th.data_ptr(), B, 0, U, out.data_ptr(), 0)
+                    if args.contract:
+                        eng.contract_device(th.data_ptr(), B, 0)
+                    else:
+                        eng.lnl_units_device(th.data_ptr(), B, 0, U, out.data_ptr(), 0)
                     e.record()
                     torch.cuda.synchronize()
+                    if args.contract:     # (the values: one lnL batch after the timed contraction)
+                        eng.lnl_units_device(th.data_ptr(), B, 0, U, out.data_ptr(), 0)
+                        torch.cuda.synchronize()
                     if r > 0:   # round 0 warms up (scratch allocation, first launches)
                         times[m].append(s.elapsed_time(e))
                     c, f = eng.refine_stats()
