@@ -50,43 +50,55 @@ constexpr bool contract2_late(int nb) { return nb <= 9; }
 
 template <int NB>
 int launch_contract2(int waves, const PsrDev& P, const double* w, const double* beta, double* s, long long s_stride,
-                     double* G, int nb_samples, hipStream_t st) {
+                     double* G, int nb_samples, hipStream_t st, const double* rho) {
   // (the dynamic-LDS attribute is set per device by set_contract_attributes)
   constexpr int CP = contract2_comp(NB);
 #ifdef EWH_DEV
   if constexpr (NB <= 10) {
     if (waves == 30) {   // (dev A/B: TwoSum accumulation)
       hipLaunchKernelGGL(HIP_KERNEL_NAME(contract2_kernel<NB, 8, CT_TWOSUM>), dim3(nb_samples), dim3(512),
-                         contract2_lds(NB), st, P, w, beta, s, s_stride, G);
+                         contract2_lds(NB), st, P, w, beta, s, s_stride, G, nullptr);
       return 0;
     }
   }
   if (waves == 35) {     // (dev A/B: the extra blocks on the first waves, round 4-5a)
     if (contract2_default_waves(NB) == 8)
       hipLaunchKernelGGL(HIP_KERNEL_NAME(contract2_kernel<NB, 8, CP, false>), dim3(nb_samples), dim3(512),
-                         contract2_lds(NB), st, P, w, beta, s, s_stride, G);
+                         contract2_lds(NB), st, P, w, beta, s, s_stride, G, nullptr);
     else
       hipLaunchKernelGGL(HIP_KERNEL_NAME(contract2_kernel<NB, 4, CP, false>), dim3(nb_samples), dim3(256),
-                         contract2_lds(NB), st, P, w, beta, s, s_stride, G);
+                         contract2_lds(NB), st, P, w, beta, s, s_stride, G, nullptr);
     return 0;
   }
 #endif
   if (waves == 0 || waves == 30) waves = contract2_default_waves(NB);
   constexpr bool LT = contract2_late(NB);
+  if constexpr (NB >= 2) {
+    if (rho) {   // the r-separated contraction (run_white decides; no ECORR, m <= 16 (NB - 1))
+      if (waves == 8)
+        hipLaunchKernelGGL(HIP_KERNEL_NAME(contract2_kernel<NB, 8, CP, LT, true>), dim3(nb_samples), dim3(512),
+                           contract2_lds(NB), st, P, w, beta, s, s_stride, G, rho);
+      else
+        hipLaunchKernelGGL(HIP_KERNEL_NAME(contract2_kernel<NB, 4, CP, LT, true>), dim3(nb_samples), dim3(256),
+                           contract2_lds(NB), st, P, w, beta, s, s_stride, G, rho);
+      return 0;
+    }
+  }
   if (waves == 8)
     hipLaunchKernelGGL(HIP_KERNEL_NAME(contract2_kernel<NB, 8, CP, LT>), dim3(nb_samples), dim3(512),
-                       contract2_lds(NB), st, P, w, beta, s, s_stride, G);
+                       contract2_lds(NB), st, P, w, beta, s, s_stride, G, nullptr);
   else
     hipLaunchKernelGGL(HIP_KERNEL_NAME(contract2_kernel<NB, 4, CP, LT>), dim3(nb_samples), dim3(256),
-                       contract2_lds(NB), st, P, w, beta, s, s_stride, G);
+                       contract2_lds(NB), st, P, w, beta, s, s_stride, G, nullptr);
   return 0;
 }
 
 int dispatch_contract2(int nb, int waves, const PsrDev& P, const double* w, const double* beta, double* s,
-                       long long s_stride, double* G, int nb_samples, hipStream_t st) {
+                       long long s_stride, double* G, int nb_samples, hipStream_t st, const double* rho) {
   int rc = 1;
   static_for<1, CONTRACT2_NB_MAX + 1>([&](auto N) {
-    if (nb == decltype(N)::value) rc = launch_contract2<decltype(N)::value>(waves, P, w, beta, s, s_stride, G, nb_samples, st);
+    if (nb == decltype(N)::value)
+      rc = launch_contract2<decltype(N)::value>(waves, P, w, beta, s, s_stride, G, nb_samples, st, rho);
   });
   if (rc == 1) return set_err(EWH_E_UNSUPPORTED, "basis too wide for the pipelined contraction (> 207 columns)");
   return rc;
@@ -100,6 +112,12 @@ int set_attr2() {
                               hipFuncAttributeMaxDynamicSharedMemorySize, (int)contract2_lds(NB)));
   EWH_HIP(hipFuncSetAttribute((const void*)contract2_kernel<NB, 8, CP, LT>,
                               hipFuncAttributeMaxDynamicSharedMemorySize, (int)contract2_lds(NB)));
+  if constexpr (NB >= 2) {
+    EWH_HIP(hipFuncSetAttribute((const void*)contract2_kernel<NB, 4, CP, LT, true>,
+                                hipFuncAttributeMaxDynamicSharedMemorySize, (int)contract2_lds(NB)));
+    EWH_HIP(hipFuncSetAttribute((const void*)contract2_kernel<NB, 8, CP, LT, true>,
+                                hipFuncAttributeMaxDynamicSharedMemorySize, (int)contract2_lds(NB)));
+  }
 #ifdef EWH_DEV
   if constexpr (NB <= 10)
     EWH_HIP(hipFuncSetAttribute((const void*)contract2_kernel<NB, 8, CT_TWOSUM>,
@@ -140,8 +158,8 @@ int launch_contract_nb(int nb, const PsrDev& P, const double* w, const double* b
 }
 
 int launch_contract2_nb(int nb, int waves, const PsrDev& P, const double* w, const double* beta, double* s,
-                        long long s_stride, double* G, int nb_samples, hipStream_t st) {
-  return dispatch_contract2(nb, waves, P, w, beta, s, s_stride, G, nb_samples, st);
+                        long long s_stride, double* G, int nb_samples, hipStream_t st, const double* rho) {
+  return dispatch_contract2(nb, waves, P, w, beta, s, s_stride, G, nb_samples, st, rho);
 }
 
 }  // namespace ewh_dev

@@ -495,15 +495,27 @@ constexpr bool ct_uses(int nb, int ws, int sh, int v, int j, bool late = true) {
 // per-tile weights); VW / WS: the virtual wave that picks the output blocks
 // (blocks VW + WS sl) and the virtual waves per sample -- WS = W SPLIT when a
 // sample's blocks are split over SPLIT workgroups (contract2_kernel).
-template <int NB, int WAVE, int W, int VW = WAVE, int WS = W, int COMP = CT_BLOCKED, bool LATE = true>
+// RSEP (round 5; the caller guarantees no ECORR and m <= 16 (NB - 1)): the
+// last block column holds only r and pad columns, so the MFMAs form the Gram
+// of the first NG = NB - 1 blocks only (C4: 78 instead of 91 blocks, -14 %),
+// and d = T^T W r is summed by VALU from the staged tile -- one FMA per
+// (row, column) on the last DW waves (column tid - 64 (W - DW)), blocked like
+// the Gram; r^T W r comes from wn_weights_kernel (rho).  The epilogue writes
+// block column NB - 1 itself: d, zeros, the pads' unit diagonal and rho.
+template <int NB, int WAVE, int W, int VW = WAVE, int WS = W, int COMP = CT_BLOCKED, bool LATE = true,
+          bool RSEP = false>
 __device__ __forceinline__ void contract2_body(const PsrDev& P, const double* __restrict__ wrow,
                                                const double* __restrict__ brow, double* __restrict__ srow,
-                                               double* __restrict__ Gout) {
+                                               double* __restrict__ Gout, const double* __restrict__ rho = nullptr) {
   extern __shared__ __attribute__((aligned(16))) double smem[];
   constexpr int LD = 16 * NB;
-  constexpr int NBLK = NB * (NB + 1) / 2;
-  constexpr int SH = ct_shape(NB, WS, LATE);          // block ownership: tiled runs (ct_order)
+  constexpr int NG = RSEP ? NB - 1 : NB;             // blocks the MFMAs form
+  constexpr int NBLK = NG * (NG + 1) / 2;
+  constexpr int SH = ct_shape(NG, WS, LATE);          // block ownership: tiled runs (ct_order)
   constexpr int SLOTS = ct_run_len(NBLK, WS, VW, LATE);
+  constexpr int DW = RSEP ? (16 * NG + 63) / 64 : 0;  // the d waves (the last DW of W)
+  constexpr bool DWAVE = RSEP && WAVE >= W - DW;
+  static_assert(!RSEP || (DW <= W && WS == W), "r-separated contraction: one workgroup per sample");
   constexpr int TILE = CT_ROWS * LD;                 // doubles per tile
   constexpr int CHUNKS = TILE * 8 / 1024;            // 1-KiB glds pieces per tile (4 NB), dealt round-robin to the W waves
   static_assert(CHUNKS * 1024 == TILE * 8, "tile must split into pieces of 1 KiB");
@@ -534,8 +546,15 @@ __device__ __forceinline__ void contract2_body(const PsrDev& P, const double* __
     hi[sl] = v4d{0.0, 0.0, 0.0, 0.0};
     lo[sl] = v4d{0.0, 0.0, 0.0, 0.0};
   }
+  // RSEP: d of column dc (the d waves), blocked like the Gram
+  const int dc = DWAVE ? min(tid - 64 * (W - DW), 16 * NG - 1) : 0;
+  double dacc = 0.0, dhi = 0.0;
   auto flush = [&]() {
     if constexpr (COMP == CT_SINGLE) return;
+    if constexpr (DWAVE) {
+      dhi += dacc;
+      dacc = 0.0;
+    }
     static_for<0, SLOTS>([&](auto SL) {
       constexpr int sl = decltype(SL)::value;
       static_for<0, 4>([&](auto R) {
@@ -553,7 +572,7 @@ __device__ __forceinline__ void contract2_body(const PsrDev& P, const double* __
     });
   };
 
-  const bool ecorr = P.n_epoch > 0;
+  const bool ecorr = !RSEP && P.n_epoch > 0;       // (RSEP: none, by the caller's choice)
   double eacc = 0.0;                                 // running s_e of column `tid`
   // pass 0: TOA rows (weights w); pass 1: epoch rows (weights -beta)
   for (int pass = 0; pass < (ecorr ? 2 : 1); ++pass) {
@@ -575,13 +594,14 @@ __device__ __forceinline__ void contract2_body(const PsrDev& P, const double* __
     // the tile's global_load_lds, so the wait for them is a counted vmcnt at
     // their use (the LDS store at the end of the iteration), never a
     // vmcnt(0) that would also wait for the next tile's DMA
-    double wraw = 0.0;
+    double wraw = 0.0, rraw = 0.0;
     int ev = -1;
     auto small = [&](int it) {
       if constexpr (WAVE == 0) {
         const int t = it * CT_ROWS + (lane & (CT_ROWS - 1));
         wraw = wsrc[min(t, nrows - 1)];
         ev = pass == 0 ? P.toa_ep[t] : -1;
+        if constexpr (RSEP) rraw = P.T[(long long)min(t, nrows - 1) * LD + LD - 1];
       }
     };
     // staged per tile by wave 0: the Gram weights; the epoch-sum weights
@@ -596,7 +616,8 @@ __device__ __forceinline__ void contract2_body(const PsrDev& P, const double* __
         const unsigned long long fmask = __ballot(fl);
         if (lane < CT_ROWS) {
           wbase[buf * CT_ROWS + lane] = w;
-          ewbase[buf * CT_ROWS + lane] = ev >= 0 ? w : 0.0;
+          // (RSEP, no ECORR: the epoch-sum weights' slot carries w r, d's row weights)
+          ewbase[buf * CT_ROWS + lane] = RSEP ? w * rraw : ev >= 0 ? w : 0.0;
         }
         if (fl) ebase[buf * CT_ROWS + __builtin_amdgcn_mbcnt_lo((unsigned)fmask, 0u)] = ev >> 1;
         if (lane == 0) fmbase[buf] = (int)(unsigned)fmask;
@@ -619,14 +640,14 @@ __device__ __forceinline__ void contract2_body(const PsrDev& P, const double* __
         const int row = 4 * kk + q;
         const double wr = wt[row];
         const double* trow = tile + row * LD + c;
-        double tv[NB], av[NB];
-        static_for<0, NB>([&](auto J) {
+        double tv[NG], av[NG];
+        static_for<0, NG>([&](auto J) {
           constexpr int j = decltype(J)::value;
-          if constexpr (ct_uses(NB, WS, SH, VW, j, LATE)) tv[j] = trow[16 * j];
-          if constexpr (ct_uses_row(NB, WS, SH, VW, j, LATE)) av[j] = wr * tv[j];
+          if constexpr (ct_uses(NG, WS, SH, VW, j, LATE)) tv[j] = trow[16 * j];
+          if constexpr (ct_uses_row(NG, WS, SH, VW, j, LATE)) av[j] = wr * tv[j];
         });
         static_for<0, SLOTS>([&](auto SL) {
-          constexpr int blk = ct_blk(NB, WS, SH, VW, decltype(SL)::value, LATE);
+          constexpr int blk = ct_blk(NG, WS, SH, VW, decltype(SL)::value, LATE);
           constexpr int bi = blk >> 6, bj = blk & 63;
           acc[decltype(SL)::value] = __builtin_amdgcn_mfma_f64_16x16x4f64(av[bi], tv[bj], acc[decltype(SL)::value], 0, 0, 0);
         });
@@ -666,6 +687,21 @@ __device__ __forceinline__ void contract2_body(const PsrDev& P, const double* __
           }
         }
       }
+      if constexpr (DWAVE) {                         // d of column dc: this tile's rows
+        const double* ewr = ewbase + cur * CT_ROWS;
+        constexpr int DR = COMP == CT_BLOCKED ? 4 : 8;     // rows per LDS trip (registers, as the epoch sums)
+#pragma unroll
+        for (int r0 = 0; r0 < CT_ROWS; r0 += DR) {
+          double tc[DR], wc[DR];
+#pragma unroll
+          for (int i = 0; i < DR; ++i) {
+            tc[i] = tile[(r0 + i) * LD + dc];
+            wc[i] = ewr[r0 + i];
+          }
+#pragma unroll
+          for (int i = 0; i < DR; ++i) dacc = fma(wc[i], tc[i], dacc);
+        }
+      }
       if ((it & (CT_GROUP - 1)) == CT_GROUP - 1 || it + 1 == ntile) flush();
       if (it + 1 < ntile) stage(cur ^ 1, it + 1);
       __syncthreads();                               // drains the glds of tile it+1 (vmcnt(0))
@@ -682,8 +718,31 @@ __device__ __forceinline__ void contract2_body(const PsrDev& P, const double* __
   }
   // epilogue: C/D layout lane -> (row q + 4r, col c); mirror to the lower half,
   // unit diagonal on pad columns (m .. LD-2) so they factor as identity.
+  if constexpr (DWAVE) {
+    // block column NB - 1: d in column LD - 1, zeros in the pad columns
+    // [16 NG, LD - 1) (their rows too); the d wave of column 0 also writes
+    // the last diagonal block: unit diagonal on the pads, rho at the corner
+    const int a = tid - 64 * (W - DW);
+    if (a < 16 * NG) {
+      const double d = COMP == CT_SINGLE ? dacc : dhi;
+      Gout[(long long)a * LD + LD - 1] = d;
+      Gout[(long long)(LD - 1) * LD + a] = d;
+#pragma unroll
+      for (int pc = 16 * NG; pc < LD - 1; ++pc) {
+        Gout[(long long)a * LD + pc] = 0.0;
+        Gout[(long long)pc * LD + a] = 0.0;
+      }
+    }
+    if (WAVE == W - DW) {
+#pragma unroll
+      for (int e = lane; e < 256; e += 64) {
+        const int row = 16 * NG + (e >> 4), col = 16 * NG + (e & 15);
+        Gout[(long long)row * LD + col] = row == LD - 1 && col == LD - 1 ? rho[blockIdx.x] : row == col ? 1.0 : 0.0;
+      }
+    }
+  }
   static_for<0, SLOTS>([&](auto SL) {
-    constexpr int blk = ct_blk(NB, WS, SH, VW, decltype(SL)::value, LATE);
+    constexpr int blk = ct_blk(NG, WS, SH, VW, decltype(SL)::value, LATE);
     constexpr int bi = blk >> 6, bj = blk & 63;
 #pragma unroll
     for (int r = 0; r < 4; ++r) {
@@ -699,10 +758,11 @@ __device__ __forceinline__ void contract2_body(const PsrDev& P, const double* __
 
 // W = 4 or 8 waves per workgroup (8: half the accumulators per wave, so the
 // narrow NB = 9 kernel fits 4 waves per SIMD and the wide NB = 13 one 2).
-template <int NB, int W, int COMP = CT_BLOCKED, bool LATE = true>
+template <int NB, int W, int COMP = CT_BLOCKED, bool LATE = true, bool RSEP = false>
 __global__ __launch_bounds__(64 * W) void contract2_kernel(PsrDev P, const double* __restrict__ w,
                                                            const double* __restrict__ beta, double* __restrict__ s,
-                                                           long long s_stride, double* __restrict__ G) {
+                                                           long long s_stride, double* __restrict__ G,
+                                                           const double* __restrict__ rho) {
   const int bl = blockIdx.x;
   const double* wrow = w + (long long)bl * P.n_toa;
   const double* brow = beta + (long long)bl * P.n_epoch;
@@ -711,7 +771,7 @@ __global__ __launch_bounds__(64 * W) void contract2_kernel(PsrDev P, const doubl
   const int wv = threadIdx.x >> 6;
   static_for<0, W>([&](auto WV) {
     constexpr int wave = decltype(WV)::value;
-    if (wv == wave) contract2_body<NB, wave, W, wave, W, COMP, LATE>(P, wrow, brow, srow, Gout);
+    if (wv == wave) contract2_body<NB, wave, W, wave, W, COMP, LATE, RSEP>(P, wrow, brow, srow, Gout, rho);
   });
 }
 // the accumulation per width: blocked from 10 blocks on (C4's 13: the same
@@ -1481,7 +1541,7 @@ int launch_contract_nb(int nb, const PsrDev& P, const double* w, const double* b
                        const double* fac, double* G, int nb_samples, hipStream_t st, double* Glo = nullptr);
 // waves: 4 or 8 per sample (0 = the measured default for nb)
 int launch_contract2_nb(int nb, int waves, const PsrDev& P, const double* w, const double* beta, double* s,
-                        long long s_stride, double* G, int nb_samples, hipStream_t st);
+                        long long s_stride, double* G, int nb_samples, hipStream_t st, const double* rho = nullptr);
 // mode: ewh_set_kernel_mode; returns 1 if no register kernel applies (caller falls back)
 int launch_chol_small(int mode, int nb, const CholJob* jobs, int B, long long u0, long long n, int b_off,
                       const double* theta, int ldth, double* units, hipStream_t st);

@@ -48,7 +48,8 @@ int set_err(int code, const std::string& msg) {
 __global__ __launch_bounds__(256) void wn_weights_kernel(PsrDev P, const double* __restrict__ theta,
                                                          int ldth, int b0, double* __restrict__ w,
                                                          double* __restrict__ beta,
-                                                         double* __restrict__ Kb, double* __restrict__ fac) {
+                                                         double* __restrict__ Kb, double* __restrict__ fac,
+                                                         double* __restrict__ rho) {
   __shared__ double red[4];
   const int bl = blockIdx.x;
   const double* th = theta + (long long)(b0 + bl) * ldth;
@@ -79,6 +80,17 @@ __global__ __launch_bounds__(256) void wn_weights_kernel(PsrDev P, const double*
   }
   acc = block_sum256(acc, red);
   if (threadIdx.x == 0) Kb[bl] = -0.5 * acc;
+  if (rho) {
+    // r^T W r (no ECORR: the r-separated contraction, contract2 RSEP): r is
+    // T_aug's last column; per thread a strided partial sum, then the tree
+    double q = 0.0;
+    for (int t = threadIdx.x; t < P.n_toa; t += 256) {
+      const double r = P.T[(long long)t * P.ld + P.ld - 1];
+      q = fma(wr[t] * r, r, q);
+    }
+    q = block_sum256(q, red);
+    if (threadIdx.x == 0) rho[bl] = q;
+  }
 }
 
 // s[bl][e][:] = sum_{t in epoch e} w_t T_aug[t][:]
@@ -1407,6 +1419,7 @@ struct DevCtx {
   size_t io_cap = 0;
   // varying-WN scratch
   double *d_w = nullptr, *d_beta = nullptr, *d_s = nullptr, *d_G = nullptr, *d_Kb = nullptr, *d_fac = nullptr;
+  double* d_rho = nullptr;       // r^T W r per sample (the r-separated contraction)
   long long s_stride = 0;     // doubles per sample in d_s (epoch rows padded to whole tiles)
   double* d_bigscr = nullptr; // chol_big_kernel: per-workgroup U blocks
   long long bigscr_cap = 0;   // workgroups per launch it holds
@@ -1816,6 +1829,7 @@ int ensure_var_scratch(DevCtx* h, int B) {
   // memory-derived limit, at most 1024): no free / re-malloc per call
   if (h->chunk > 0 && (h->chunk >= B || h->chunk >= h->chunk_cap)) return 0;
   for (void* p : {(void*)h->d_w, (void*)h->d_beta, (void*)h->d_s, (void*)h->d_G, (void*)h->d_Kb, (void*)h->d_fac,
+                  (void*)h->d_rho,
                   (void*)h->d_Glo}) {
     if (p) {
       (void)hipFree(p);
@@ -1854,6 +1868,7 @@ int ensure_var_scratch(DevCtx* h, int B) {
   h->s_stride = (long long)sstride;
   if ((rc = dalloc(h, &h->d_G, chunk * maxld * maxld))) return rc;
   if ((rc = dalloc(h, &h->d_Kb, chunk))) return rc;
+  if ((rc = dalloc(h, &h->d_rho, chunk))) return rc;
   if ((rc = dalloc(h, &h->d_fac, chunk * maxfac))) return rc;
   h->d_Glo = nullptr;
   if (wide && (rc = dalloc(h, &h->d_Glo, chunk * maxld * maxld))) return rc;
@@ -1874,15 +1889,24 @@ int ensure_var_scratch(DevCtx* h, int B) {
 // white-noise terms of one pulsar for samples [b0, b0 + nb) into the chunk scratch
 int run_white(DevCtx* h, int p, const double* theta, int ldth, int b0, int nb) {
   PsrHost& ps = h->psr[p];
+  const bool c2 = ps.dev.n_bgroup == 0 && h->kernel_mode != 7 && ps.nb <= CONTRACT2_NB_MAX;
+  // the r-separated contraction (contract2 RSEP): when the residual alone
+  // fills the last 16-column block (m <= 16 (NB - 1): C4's 192 columns + r
+  // = 13 blocks), the MFMAs form only the NB - 1 block Gram; d = T^T W r by
+  // VALU from the staged tiles, r^T W r in wn_weights_kernel.  No ECORR
+  // (the epoch pass would need the same split).  Dev mode 36: off (A/B)
+  const bool rsep = c2 && ps.dev.n_epoch == 0 && ps.nb >= 2 && ps.dev.m <= 16 * (ps.nb - 1) &&
+                    h->kernel_mode != 36 && h->kernel_mode != 30;
   hipLaunchKernelGGL(wn_weights_kernel, dim3(nb), dim3(256), 0, h->stream, ps.dev, theta, ldth, b0, h->d_w,
-                     h->d_beta, h->d_Kb, h->d_fac);
-  if (ps.dev.n_bgroup == 0 && h->kernel_mode != 7 && ps.nb <= CONTRACT2_NB_MAX) {
+                     h->d_beta, h->d_Kb, h->d_fac, rsep ? h->d_rho : nullptr);
+  if (c2) {
     // (dev library A/B: mode 15 = 4 waves per sample, mode 16 = 8)
     // (30: TwoSum accumulation up to 10 blocks)
     // (35: the run remainder on the first waves, as in round 4-5a)
     const int waves = h->kernel_mode == 15 ? 4 : h->kernel_mode == 16 ? 8 : h->kernel_mode == 30 ? 30
                     : h->kernel_mode == 35 ? 35 : 0;
-    int rc = launch_contract2_nb(ps.nb, waves, ps.dev, h->d_w, h->d_beta, h->d_s, h->s_stride, h->d_G, nb, h->stream);
+    int rc = launch_contract2_nb(ps.nb, waves, ps.dev, h->d_w, h->d_beta, h->d_s, h->s_stride, h->d_G, nb, h->stream,
+                                 rsep ? h->d_rho : nullptr);
     if (rc) return rc;
     EWH_HIP(hipGetLastError());
     return 0;
@@ -1940,7 +1964,7 @@ int setup_fixed(DevCtx* h) {
   for (int p = 0; p < h->P; ++p) {
     PsrHost& ps = h->psr[p];
     hipLaunchKernelGGL(wn_weights_kernel, dim3(1), dim3(256), 0, h->stream, ps.dev, dummy_theta, 0, 0, w, beta, Kb,
-                       nullptr);
+                       nullptr, nullptr);
     if (ps.n_epoch > 0)
       hipLaunchKernelGGL(epoch_sums_kernel, dim3(ps.n_epoch, 1), dim3(256), 0, h->stream, ps.dev, w, nullptr, s);
     if (ps.dev.n_bgroup == 0 && h->kernel_mode != 7) {
@@ -3313,14 +3337,14 @@ int ewh_set_fixed_white(ewh_handle* H, const double* values) {
 }
 
 int ewh_set_kernel_mode(ewh_handle* H, int32_t mode) {
-  if (!H || mode < 0 || mode > 35) return set_err(EWH_E_INVALID, "bad handle / mode");
+  if (!H || mode < 0 || mode > 36) return set_err(EWH_E_INVALID, "bad handle / mode");
 #ifdef EWH_DEV
   constexpr bool dev_lib = true;   // mode 33 (the one-proposal C5 schedule with the diagonal launched apart)
 #else
   constexpr bool dev_lib = false;
 #endif
   if (mode != 0 && mode != 1 && mode != 2 && mode != 7 && mode != MODE_WIDE && mode != MODE_DD && !variant_built(mode) &&
-      !((mode == 33 || mode == MODE_WIDE_R05A || mode == 35) && dev_lib))
+      !((mode == 33 || mode == MODE_WIDE_R05A || mode == 35 || mode == 36) && dev_lib))
     return set_err(EWH_E_UNSUPPORTED, "kernel mode " + std::to_string(mode) +
                                           " is not built into this library (A/B variants: the dev library, make dev)");
   for (DevCtx* h : H->ctx) {
