@@ -113,6 +113,49 @@ __global__ __launch_bounds__(256) void epoch_sums_kernel(PsrDev P, const double*
   }
 }
 
+// The same for ES_S samples per workgroup (round 5, the varying-white-noise
+// wide path: the per-(epoch, sample) kernel above re-read the epoch's T rows
+// from L2 / MALL for every sample -- 1.0 ms per 256 samples at 384 columns x
+// 10k TOAs, 8 % of the w372 batch): the epoch's rows of each column are read
+// once into registers (ES_R at a time), the group's weights staged in LDS
+// (epochs up to ES_RMAX TOAs; longer ones, and theta-dependent bases, keep
+// the kernel above).  s[b][e][c] = sum_t w_bt T[t][c], the terms in TOA
+// order by fma.
+constexpr int ES_S = 32, ES_R = 16, ES_RMAX = 128;
+__global__ __launch_bounds__(256) void epoch_sums_multi_kernel(PsrDev P, const double* __restrict__ w, int nsamp,
+                                                               double* __restrict__ s) {
+  __shared__ double ws[ES_S * ES_RMAX];
+  const int e = blockIdx.x, s0 = blockIdx.y * ES_S;
+  const int t0 = P.ep_start[e], nr = P.ep_stop[e] - t0;
+  const int ns = min(ES_S, nsamp - s0);
+  for (int i = threadIdx.x; i < ES_S * nr; i += 256) {
+    const int sl = i / nr, r = i - sl * nr;
+    ws[sl * ES_RMAX + r] = sl < ns ? w[(long long)(s0 + sl) * P.n_toa + t0 + r] : 0.0;
+  }
+  __syncthreads();
+  for (int c = threadIdx.x; c < P.ld; c += 256) {
+    double acc[ES_S];
+#pragma unroll
+    for (int sl = 0; sl < ES_S; ++sl) acc[sl] = 0.0;
+    for (int r0 = 0; r0 < nr; r0 += ES_R) {
+      double tv[ES_R];
+#pragma unroll
+      for (int r = 0; r < ES_R; ++r) tv[r] = r0 + r < nr ? P.T[(long long)(t0 + r0 + r) * P.ld + c] : 0.0;
+      const int rn = min(ES_R, nr - r0);
+#pragma unroll
+      for (int sl = 0; sl < ES_S; ++sl) {
+        const double* wl = ws + sl * ES_RMAX + r0;
+#pragma unroll
+        for (int r = 0; r < ES_R; ++r)
+          if (r < rn) acc[sl] = fma(wl[r], tv[r], acc[sl]);
+      }
+    }
+#pragma unroll
+    for (int sl = 0; sl < ES_S; ++sl)
+      if (sl < ns) s[((long long)(s0 + sl) * P.n_epoch + e) * P.ld + c] = acc[sl];
+  }
+}
+
 // ----------------------------------------------------------------------------
 // fixed white noise, one-off (ewh_create / ewh_set_fixed_white): the cached
 // Gram G = T_aug^T W T_aug - sum_e beta_e s_e s_e^T with every entry summed
@@ -1369,6 +1412,7 @@ constexpr size_t LDS_MAX = 160 * 1024;
 
 struct PsrHost {
   int n_toa = 0, m = 0, nlead = 0, ld = 0, nb = 0, n_epoch = 0;
+  int max_epoch = 0;               // TOAs of the longest ECORR epoch
   int fx_m = 0, fx_ld = 0, fx_nb = 0;
   int ncommon = 0, nloc = 0, gstart = 0;   // correlated layout of the reduced matrix
   // correlated common process with varying white noise: T_aug is laid out
@@ -1911,9 +1955,15 @@ int run_white(DevCtx* h, int p, const double* theta, int ldth, int b0, int nb) {
     EWH_HIP(hipGetLastError());
     return 0;
   }
-  if (ps.n_epoch > 0)
-    hipLaunchKernelGGL(epoch_sums_kernel, dim3(ps.n_epoch, nb), dim3(256), 0, h->stream, ps.dev, h->d_w, h->d_fac,
-                       h->d_s);
+  if (ps.n_epoch > 0) {
+    // (dev mode 37: one sample per workgroup, as in round 5a)
+    if (ps.dev.n_bgroup == 0 && ps.max_epoch <= ES_RMAX && h->kernel_mode != 37)
+      hipLaunchKernelGGL(epoch_sums_multi_kernel, dim3(ps.n_epoch, (nb + ES_S - 1) / ES_S), dim3(256), 0, h->stream,
+                         ps.dev, h->d_w, nb, h->d_s);
+    else
+      hipLaunchKernelGGL(epoch_sums_kernel, dim3(ps.n_epoch, nb), dim3(256), 0, h->stream, ps.dev, h->d_w, h->d_fac,
+                         h->d_s);
+  }
   int rc = launch_contract_nb(ps.nb, ps.dev, h->d_w, h->d_beta, h->d_s, h->d_fac, h->d_G, nb, h->stream,
                               ps.nb > BIG_NB_MAX ? h->d_Glo : nullptr);
   if (rc) return rc;
@@ -2487,6 +2537,8 @@ int create_ctx(const ewh_pta_desc* d, const std::vector<ProjCoef>& proj, int dev
     ps.nb = nb_for(ps.m + 1);
     ps.ld = 16 * ps.nb;
     ps.n_epoch = s.n_epoch;
+    ps.max_epoch = 0;
+    for (int e = 0; e < s.n_epoch; ++e) ps.max_epoch = std::max(ps.max_epoch, s.epoch_stop[e] - s.epoch_start[e]);
     ps.fx_m = s.n_col - s.n_lead_const;
     ps.ncommon = d->common ? s.n_common : 0;
     ps.nloc = ps.fx_m - ps.ncommon;
@@ -3337,14 +3389,14 @@ int ewh_set_fixed_white(ewh_handle* H, const double* values) {
 }
 
 int ewh_set_kernel_mode(ewh_handle* H, int32_t mode) {
-  if (!H || mode < 0 || mode > 36) return set_err(EWH_E_INVALID, "bad handle / mode");
+  if (!H || mode < 0 || mode > 37) return set_err(EWH_E_INVALID, "bad handle / mode");
 #ifdef EWH_DEV
   constexpr bool dev_lib = true;   // mode 33 (the one-proposal C5 schedule with the diagonal launched apart)
 #else
   constexpr bool dev_lib = false;
 #endif
   if (mode != 0 && mode != 1 && mode != 2 && mode != 7 && mode != MODE_WIDE && mode != MODE_DD && !variant_built(mode) &&
-      !((mode == 33 || mode == MODE_WIDE_R05A || mode == 35 || mode == 36) && dev_lib))
+      !((mode == 33 || mode == MODE_WIDE_R05A || mode == 35 || mode == 36 || mode == 37) && dev_lib))
     return set_err(EWH_E_UNSUPPORTED, "kernel mode " + std::to_string(mode) +
                                           " is not built into this library (A/B variants: the dev library, make dev)");
   for (DevCtx* h : H->ctx) {

@@ -313,7 +313,10 @@ int ewh_refine_stats(ewh_handle* h, int64_t* checked, int64_t* refined);
  * 5a (separate forward and reversed fp64 launches, 128 MB scratch budgets
  * that cap the launches at 56-624 workgroups), 35 = the varying-white-noise
  * contraction with the blocks' remainder on the first waves (round 4-5a:
- * the waves that also form the ECORR epoch sums).  Other modes return
+ * the waves that also form the ECORR epoch sums), 36 = the contraction
+ * without the r-separated Gram (r in the MFMA blocks, as before round 5h),
+ * 37 = the wide path's ECORR epoch sums one sample per workgroup (as before
+ * round 5h).  Other modes return
  * EWH_E_UNSUPPORTED. */
 int ewh_set_kernel_mode(ewh_handle* h, int32_t mode);
 
