@@ -1468,6 +1468,7 @@ struct DevCtx {
   double* d_bigscr = nullptr; // chol_big_kernel: per-workgroup U blocks
   long long bigscr_cap = 0;   // workgroups per launch it holds
   int bigscr_nb = 0;
+  long long scr_budget = 0;      // bytes for each of the wide / dd scratches (scratch_budget)
   double* d_widescr = nullptr;   // chol_wide_kernel: per-workgroup U blocks
   long long widescr_len = 0;     // doubles
   double* d_ddscr = nullptr;     // chol_dd_kernel: per-workgroup hi / lo matrices
@@ -1703,7 +1704,20 @@ bool dd_path(const DevCtx* h, int nb, bool fixed) {
 // 24 blocks (600 KB) on 218 waves per launch.  Dev mode 34 keeps the 128 MB
 // budgets and the separate forward / reversed launches (A/B).
 constexpr int MODE_WIDE_R05A = 34;
-long long scratch_budget(const DevCtx* h) { return h->kernel_mode == MODE_WIDE_R05A ? (1LL << 27) : (1LL << 32); }
+// (capped at an eighth of the device memory free when first sized, so several
+// handles on one device -- multi-context tests, one handle per sampler
+// thread -- cannot take it all; at least the round-5a 128 MB)
+long long scratch_budget(DevCtx* h) {
+  if (h->kernel_mode == MODE_WIDE_R05A) return 1LL << 27;
+  if (h->scr_budget == 0) {
+    size_t fr = 0, tot = 0;
+    (void)hipSetDevice(h->device);
+    h->scr_budget = hipMemGetInfo(&fr, &tot) == hipSuccess
+                        ? std::max<long long>(1LL << 27, std::min<long long>(1LL << 32, (long long)(fr / 8)))
+                        : (1LL << 27);
+  }
+  return h->scr_budget;
+}
 
 long long ensure_dd_scratch(DevCtx* h, int ld) {
   const long long per = dd_scratch_per_wg(ld);
