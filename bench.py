@@ -473,6 +473,10 @@ def main():
                     help="c5 only: shard samples (no exchange) or pulsars (all-gather of the kept common blocks, "
                          "then the dense factorisation on every rank: one proposal over N GPUs)")
     ap.add_argument("--c5-batch", type=int, default=None, help="c5 proposals per step (default 512 / 1 for pulsars)")
+    ap.add_argument("--c3-partition", default="units", choices=["units", "samples"],
+                    help="c3: units = contiguous (pulsar-major) unit ranges of equal cost per rank + one RCCL "
+                         "all-reduce of the B-vector per step (default); samples = every rank evaluates all "
+                         "pulsars for its own batch_per_gpu proposals, no collective (SURVEY.md 8(e): report both)")
     ap.add_argument("--dist-backend", default="nccl", choices=["nccl", "gloo"],
                     help="nccl (= RCCL, the default); gloo only to rehearse the multi-rank path")
     ap.add_argument("--same-device", action="store_true",
@@ -535,15 +539,26 @@ def main():
     theta = torch.from_numpy(X).to(dev)
     eng = pta.engine(device=dev.index)
     eng.set_kernel_mode(args.kernel_mode)
-    costs = eng.unit_costs()
-    ranges = sharding.unit_ranges(costs, B, world)
-    u0, u1 = ranges[rank]
+    P = len(pta.signal_collections)
+    samples = args.c3_partition == "samples"
+    if samples:
+        # replicas: rank r takes proposals [r bpg, (r + 1) bpg) of the global
+        # batch, all pulsars, and needs no exchange (its lnL are complete)
+        bl = args.batch_per_gpu
+        theta = theta[rank * bl:(rank + 1) * bl].contiguous()
+        ranges = [(r * bl, (r + 1) * bl) for r in range(world)]     # (sample ranges)
+        B_run, u0, u1 = bl, 0, P * bl
+    else:
+        costs = eng.unit_costs()
+        ranges = sharding.unit_ranges(costs, B, world)
+        B_run = B
+        u0, u1 = ranges[rank]
     stream = torch.cuda.current_stream(dev)
     # two output buffers: the all-reduce of step i (RCCL's stream) overlaps
     # the likelihood launch of step i+1 (this stream); step i+2 reuses the
     # buffer only after that all-reduce (work.wait(): a stream dependency for
     # RCCL, not a host wait)
-    outs = [torch.zeros(B, dtype=torch.float64, device=dev) for _ in range(2)]
+    outs = [torch.zeros(B_run, dtype=torch.float64, device=dev) for _ in range(2)]
     works = [None, None]
 
     def step(i, ev=None):
@@ -553,10 +568,10 @@ def main():
             works[k] = None
         if ev is not None:
             ev[0].record(stream)
-        eng.lnl_units_device(theta.data_ptr(), B, u0, u1, outs[k].data_ptr(), stream.cuda_stream)
+        eng.lnl_units_device(theta.data_ptr(), B_run, u0, u1, outs[k].data_ptr(), stream.cuda_stream)
         if ev is not None:
             ev[1].record(stream)
-        if world > 1:
+        if world > 1 and not samples:
             works[k] = dist.all_reduce(outs[k], async_op=True)
 
     def drain():
@@ -595,7 +610,7 @@ def main():
     if args.verify and rank == 0:
         # the reduced batch against the single-device entry (ewh_lnl_batch,
         # pulsar-order device fold) on its first samples: strict bound
-        nv = min(B, 256)
+        nv = min(B_run, 256)
         ref = pta.get_lnlikelihood_batch(X[:nv])
         fin = np.isfinite(ref)
         same_inf = bool(np.array_equal(fin, np.isfinite(lnl[:nv])))
@@ -609,7 +624,7 @@ def main():
     f_unit = algorithmic_flops_per_unit(m_psr)
     flops = 0.0
     for p in range(len(m_psr)):
-        lo, hi = max(u0, p * B), min(u1, (p + 1) * B)
+        lo, hi = max(u0, p * B_run), min(u1, (p + 1) * B_run)
         flops += max(0, hi - lo) * f_unit[p]
     achieved = flops / (launch_ms * 1e-3) / 1e12
     # HBM bytes per launch of this kernel from the committed PMC pass, used
@@ -645,12 +660,14 @@ def main():
             "config": {"workload": "C3: 45 psr, n=2000..20000 TOAs (495k) over 14.7 yr, ECORR, RN+DM 30 freqs, "
                                    "CURN 14 freqs merged, fixed white noise (TNT cached), basis m=132",
                        "global_batch": B, "batch_per_gpu": args.batch_per_gpu, "n_pulsars": len(m_psr),
-                       "parallelism": f"units{world}", "finite_fraction": float(np.mean(np.isfinite(lnl)))},
+                       "parallelism": f"{'samples' if samples else 'units'}{world}",
+                       "finite_fraction": float(np.mean(np.isfinite(lnl)))},
             "rccl_world": rccl_world,
             "dist": {"backend": args.dist_backend if world > 1 else None, "same_device": bool(args.same_device),
                      "launcher": "bench.py" if os.environ.get(LAUNCHER_ENV) else
                      ("torchrun" if os.environ.get("TORCHELASTIC_RUN_ID") else None),
-                     "unit_ranges": [list(r) for r in ranges],
+                     "partition": args.c3_partition,
+                     ("sample_ranges" if samples else "unit_ranges"): [list(r) for r in ranges],
                      "rank_elapsed_s": per_rank[:, 0].tolist(), "rank_launch_ms": per_rank[:, 1].tolist()},
             "roofline": {"bound": "mfma", "achieved": achieved, "peak": FP64_MFMA_PEAK_TFLOPS, "unit": "TFLOP/s",
                          "frac": achieved / FP64_MFMA_PEAK_TFLOPS, "traffic": traffic, "traffic_source": traffic_src,
