@@ -35,6 +35,8 @@
 // log d_p summed per pivot; the last pivot is q = r^T N^-1 r - d^T Sigma^-1 d.
 #include "ewarp_dev.h"
 
+#include <cstdlib>
+
 namespace ewh_dev {
 namespace {
 
@@ -135,8 +137,10 @@ __device__ __forceinline__ void dd_factor_diag(const DdLds<PW>& S, int r0, int n
 template <int PW, bool RSOLVE>
 __device__ __forceinline__ void chol_ddb_unit(const CholJob* __restrict__ jobs, int B, long long u, int b_off,
                               const double* __restrict__ theta, double* __restrict__ out_units,
-                              double* __restrict__ scratch, long long scr_per_wg, double2* lds) {
-  // (theta: the unit's own row)
+                              double* __restrict__ scratch, long long scr_per_wg, double2* lds, int dbg) {
+  // (theta: the unit's own row; dbg: dev timing probe only -- bit 0 skips the
+  // trailing update, bit 1 the panel solve, bit 2 wave 0's diagonal chain;
+  // the results are then meaningless.  0 in the product)
   const int tid = threadIdx.x, wave = tid >> 6, lane = tid & 63;
   // (uniform: the job's fields load into scalar registers, not 50 VGPRs)
   const int p_ = __builtin_amdgcn_readfirstlane((int)(u / B)), b = __builtin_amdgcn_readfirstlane((int)(u % B));
@@ -190,7 +194,7 @@ __device__ __forceinline__ void chol_ddb_unit(const CholJob* __restrict__ jobs, 
     const int t0 = r0 + PW, m = n - t0;
     // A. panel solve by forward substitution, one thread per column j:
     // U[p][j] = s_p (A[r0 + p][j] - sum_{r < p} U_kk[r][p] U[r][j])
-    for (int jj = tid; jj < m; jj += DD_THREADS) {
+    for (int jj = tid; jj < ((dbg & 2) ? 0 : m); jj += DD_THREADS) {
       const int j = t0 + jj;
       dd a[PW];
 #pragma unroll
@@ -259,11 +263,11 @@ __device__ __forceinline__ void chol_ddb_unit(const CholJob* __restrict__ jobs, 
           }
       }
       lds_wave_sync();
-      dd_factor_diag<PW>(S, t0, n, lane, ldet, ok, qv);
+      if (!(dbg & 4)) dd_factor_diag<PW>(S, t0, n, lane, ldet, ok, qv);
     } else {
       constexpr int QD = PW / 4;                 // 4x4 tiles inside the next diagonal block
       const int ntiles = T * (T + 1) / 2;
-      for (int idx = tid - 64; idx < ntiles; idx += DD_THREADS - 64) {
+      for (int idx = tid - 64; idx < ((dbg & 1) ? 0 : ntiles); idx += DD_THREADS - 64) {
         int ti, tj;
         tri_decode(T, idx, ti, tj);
         if (tj < QD) continue;                   // (wave 0's)
@@ -327,14 +331,14 @@ __global__ __launch_bounds__(DD_THREADS) void chol_dd_kernel(const CholJob* __re
                                                              double* __restrict__ out_units,
                                                              double* __restrict__ scratch, long long scr_per_wg,
                                                              const int* __restrict__ list,
-                                                             const int* __restrict__ count) {
+                                                             const int* __restrict__ count, int dbg) {
   extern __shared__ __attribute__((aligned(16))) double2 dd_smem[];
   // one call site (the unit body is inlined once)
   const int cnt = list ? *count : (int)gridDim.x;
   for (int i = blockIdx.x; i < cnt; i += gridDim.x) {
     const long long u = list ? (long long)list[i] : u0 + i;
     chol_ddb_unit<PW, RSOLVE>(jobs, B, u, b_off, theta + (long long)(u % B) * ldth, out_units, scratch, scr_per_wg,
-                              dd_smem);
+                              dd_smem, dbg);
   }
 }
 
@@ -364,12 +368,16 @@ template <int PW>
 void launch_dd(const CholJob* jobs, int B, long long u0, int b_off, const double* theta, int ldth, double* units,
                double* scr, long long scr_per_wg, unsigned grid, const int* list, const int* count, int ld,
                hipStream_t st, bool r05a) {
+  int dbg = 0;
+#ifdef EWH_DEV
+  if (const char* e = getenv("EWARP_DD_SKIP")) dbg = atoi(e);   // (dev timing probe, scripts only)
+#endif
   if (r05a)
     hipLaunchKernelGGL(HIP_KERNEL_NAME(chol_dd_kernel<PW, false>), dim3(grid), dim3(DD_THREADS), dd_lds<PW>(ld), st,
-                       jobs, B, u0, b_off, theta, ldth, units, scr, scr_per_wg, list, count);
+                       jobs, B, u0, b_off, theta, ldth, units, scr, scr_per_wg, list, count, dbg);
   else
     hipLaunchKernelGGL(HIP_KERNEL_NAME(chol_dd_kernel<PW, true>), dim3(grid), dim3(DD_THREADS), dd_lds<PW>(ld), st,
-                       jobs, B, u0, b_off, theta, ldth, units, scr, scr_per_wg, list, count);
+                       jobs, B, u0, b_off, theta, ldth, units, scr, scr_per_wg, list, count, dbg);
 }
 
 int launch_dd_any(const CholJob* jobs, int B, long long u0, int b_off, const double* theta, int ldth, double* units,
