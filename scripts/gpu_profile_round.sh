@@ -26,7 +26,9 @@ pmc() {  # pmc <name> <script args> -- counters...
 # the PMC passes run scripts/chol_ab.py, which loads the dev library: build
 # (or confirm up to date) both libraries first, so a stale or missing dev
 # build stops the profile here instead of after the bench
-run make 600 make -C enterprise_warp_amd/csrc -j16 all dev
+# (SKIP_MAKE=1: use the libraries built in-tree before the upload -- build/obj
+# does not travel, so make would rebuild both from scratch on the box)
+[ "${SKIP_MAKE:-0}" = 1 ] || run make 600 make -C enterprise_warp_amd/csrc -j16 all dev
 test -f enterprise_warp_amd/libewarp_hip_dev.so || { echo "dev library missing: stopping"; exit 1; }
 python -c "import bench; print('kernel sources sha', bench.kernel_sources_sha())" > gpurun_out/kernel_sources_sha_$TAG.txt
 cp gpurun_out/kernel_sources_sha_$TAG.txt gpurun_out/pmc_${TAG}_sha.txt   # (read by scripts/pmc_summary.py)
