@@ -1,4 +1,4 @@
-"""Contraction PMC summary of a round profile (scripts/gpu_final.sh TAG):
+"""Contraction PMC summary of a round profile (scripts/gpu_profile_round.sh TAG):
 fp64 MFMA-busy fraction and HBM read rate of contract2_kernel on C2 / C4 from
 gpurun_out/cpmc_<TAG>_{busy,fetch,write}, written to
 profiles/<TAG>/contraction_pmc.json.

@@ -1,4 +1,4 @@
-# Final-tree checks on one GPU (round 5): the -m gpu suite, the dev A/B
+# Final-tree checks on one GPU: the -m gpu suite, the dev A/B
 # suite (-m gpu_ab), smoke, and the 2-rank launcher rehearsal in both C3
 # partitions.  Outputs under gpurun_out/ tagged TAG; stops at a crash.
 set -u
