@@ -234,7 +234,7 @@ __device__ __forceinline__ void contract_xr_body(const PsrDev& P, const double* 
   const double* ti_p = P.T + 16 * bi + c;
   const double* tj_p = P.T + 16 * bj + c;
   double na0, na1, nti, ntj;
-  auto load = [&](int t0) {
+  auto load = [&](int t0) {            // (the last k-steps: rows clamped)
     const int row = t0 + q;
     const int rw = min(row, n - 1), rt = min(row, n);
     na0 = w0[rw];
@@ -242,14 +242,34 @@ __device__ __forceinline__ void contract_xr_body(const PsrDev& P, const double* 
     nti = ti_p[(long long)rt * LD];
     ntj = tj_p[(long long)rt * LD];
   };
-  load(0);
+  // Every other k-step (rows t0 + q < n): wave-uniform bases w + t0 and
+  // T + t0 LD plus per-lane 32-bit byte offsets fixed for the whole loop, so
+  // the loads take the SGPR-base form and a step costs no VALU address
+  // arithmetic (round 5h: the clamped 64-bit form above spent ~20 VALU per
+  // 8 MFMAs on addresses -- PMC 5.4 VALU per MFMA, 0.70 MFMA-busy).  w_off
+  // is the caller's guarantee (nsamp n 8 < 4 GB).
+  const unsigned wo0 = (unsigned)((min(s0 + c, nsamp - 1) * (long long)n + q) * 8);
+  const unsigned wo1 = (unsigned)((min(s0 + 16 + c, nsamp - 1) * (long long)n + q) * 8);
+  const unsigned toi = (unsigned)((q * LD + 16 * bi + c) * 8), toj = (unsigned)((q * LD + 16 * bj + c) * 8);
+  auto load_fast = [&](int t) {
+    const char* wb = (const char*)(w + t);
+    const char* tb = (const char*)(P.T + (long long)t * LD);
+    na0 = *(const double*)(wb + wo0);
+    na1 = *(const double*)(wb + wo1);
+    nti = *(const double*)(tb + toi);
+    ntj = *(const double*)(tb + toj);
+  };
+  if (n >= 4) load_fast(0); else load(0);
   // (the flush outside the k-step loop: the accumulators stay in the MFMA's
   // registers for a whole group instead of moving around every MFMA)
   for (int g0 = 0; g0 < n; g0 += XR_GROUP) {
     const int g1 = min(g0 + XR_GROUP, n);
     for (int t0 = g0; t0 < g1; t0 += 4) {
       const double a0 = na0, a1 = na1, ti = nti, tj = ntj;
-      if (t0 + 4 < n) load(t0 + 4);
+      if (t0 + 8 <= n)
+        load_fast(t0 + 4);
+      else if (t0 + 4 < n)
+        load(t0 + 4);
       static_for<0, 4>([&](auto X) {
         constexpr int x = decltype(X)::value;
         const double bx = tj * row_newbcast<4 * V + x>(ti);
@@ -312,7 +332,8 @@ int launch_contract_wide(int nb, const PsrDev& P, const double* w, const double*
   const int nblk = nb * (nb + 1) / 2;
   // no theta-dependent columns: the TOA term as one GEMM over the batch,
   // then the ECORR term per sample onto it (or nothing, without epochs)
-  const bool xr = P.n_bgroup == 0 && !contract_wide_only();
+  // (the batch GEMM addresses the chunk's weights with 32-bit byte offsets)
+  const bool xr = P.n_bgroup == 0 && !contract_wide_only() && (long long)nb_samples * P.n_toa * 8 < (1LL << 32);
   if (xr) {
     const unsigned groups = (unsigned)((nb_samples + XR_S - 1) / XR_S);
     hipLaunchKernelGGL(contract_xr_kernel, dim3(groups * (unsigned)nblk), dim3(256), 0, st, P, w, nb_samples, G, Glo);
