@@ -359,3 +359,26 @@ def test_system_noise_prior_draws(require_gpu):
     ent, ext = reference_lnl(pta, X, exact="dd")
     check_accuracy(got, ent, ext, "c1_system model, 16 prior draws", per_sample=True)
     _route_vs_dd(pta, X, got, "c1_system model, 16 prior draws")
+
+
+def test_wide_long_epochs_vs_oracle(require_gpu):
+    """The wide varying-white-noise path with ECORR epochs of 100 TOAs (the
+    1 s quantisation limit of the synthetic 0.01 s channel spacing): the
+    multi-sample epoch sums (epoch_sums_multi_kernel) take each epoch's rows
+    in 16-row register chunks, the last one partial; near-truth draws against
+    the enterprise-order oracle at the strict bound (EcorrKernelNoise,
+    enterprise_models.py:133-146, on a 60-frequency basis,
+    enterprise_models.py:148-167)."""
+    psr = synth.make_pulsar("J0000+0100", 2000, seed=101, epoch_size=100)
+    terms = {"efac": "by_backend", "equad": "by_backend", "ecorr": "by_backend",
+             "spin_noise": "powerlaw_60_nfreqs", "dm_noise": "powerlaw_60_nfreqs", "chromred": "4_60_nfreqs"}
+    ns = synth.params_namespace(psr.toas.max() - psr.toas.min(), False)
+    pta = synth.build_pta([psr], terms, {}, ns, None)
+    epochs = pta.signal_collections[0].ecorr_epochs()
+    assert max(e[1] - e[0] for e in epochs) > 64 and pta.signal_collections[0].T.shape[1] > 16 * 16
+    truth = synth.truth_values(pta, 102, white=synth.white_noisedict([psr], 103))
+    synth.simulate_residuals(pta, truth, 104)
+    X = synth.near_draws(pta, truth, 6, 105)
+    got = pta.get_lnlikelihood_batch(X)
+    assert np.all(np.isfinite(got))
+    check_parity(got, oracle_lnl(pta, X), "wide basis, 100-TOA ECORR epochs, sampled white noise")
