@@ -1689,9 +1689,11 @@ constexpr int MODE_WIDE = 27, MODE_DD = 29;
 // instead, mode 1 to the LDS kernel (A/B)
 // (MODE_DD: every unit in double-double; the default: verify-and-refine --
 // the forward and the reversed-order fp64 chol_wide factorisations, and
-// chol_dd_kernel only for the units on which they disagree by more than a
-// quarter of the strict bound: near-truth draws stay on fp64 MFMA, the
-// ill-conditioned prior draws get the double-double value)
+// chol_dd_kernel only for the units on which they disagree by more than
+// 1/16 of the strict bound (VERIFY_FRAC, chol_dd.hip; 1/4 until r05j let 5 of
+// 4096 system-model prior draws through at up to 4.4x strict from double-
+// double): near-truth draws stay on fp64 MFMA, the ill-conditioned prior
+// draws get the double-double value)
 bool dd_path(const DevCtx* h, int nb, bool fixed) {
   if (h->corr || h->osmode || h->kernel_mode == MODE_WIDE || h->kernel_mode == 1) return false;
   return nb > BIG_NB_MAX || (fixed && nb > MFMA_NB_MAX);

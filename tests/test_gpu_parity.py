@@ -382,3 +382,31 @@ def test_wide_long_epochs_vs_oracle(require_gpu):
     got = pta.get_lnlikelihood_batch(X)
     assert np.all(np.isfinite(got))
     check_parity(got, oracle_lnl(pta, X), "wide basis, 100-TOA ECORR epochs, sampled white noise")
+
+
+@pytest.mark.parametrize("case", ["system", "w372_fixed"])
+def test_verify_route_matches_dd_at_scale(require_gpu, case):
+    """The verify-and-refine route against double-double everywhere (kernel
+    mode 29) on the bench's whole prior-draw batches -- 4096 draws of the
+    reference's system_noise_example model, 1024 of the 372-column pulsar --
+    at the strict bound on every sample: two fp64 orders that agree while both
+    are wrong would show here (the call matched: pta.get_lnlikelihood,
+    bilby_warp.py:35)."""
+    import os
+    from conftest import ROOT
+    if case == "system":
+        cfg = synth.config_system(os.path.join(ROOT, "tests", "golden", "ref_examples"))
+    else:
+        cfg = synth.config_wide(True)
+    pta = cfg.pta
+    X = synth.prior_draws(pta, cfg.B, cfg.theta_seed)
+    eng = pta.engine()
+    got = pta.get_lnlikelihood_batch(X)
+    c, r = eng.refine_stats()
+    assert r > 0, "no unit refined: the route was not exercised"
+    eng.set_kernel_mode(29)
+    try:
+        dd = pta.get_lnlikelihood_batch(X)
+    finally:
+        eng.set_kernel_mode(0)
+    check_parity(got, dd, f"{case}: verify-and-refine route vs double-double, {cfg.B} prior draws")
