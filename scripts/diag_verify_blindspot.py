@@ -6,7 +6,7 @@ bound, each against the CPU double-double reference (oracle/ddref.py) and
 enterprise's own fp64 order; plus the forward / reversed fp64 pass values
 (mode 27 and the verify's own agreement) for those samples.
 
-    python scripts/diag_verify_blindspot.py [system|w372_fixed] [--max 12]
+    python scripts/diag_verify_blindspot.py [system|w372_fixed] [--max 12] [--seed-offset 0]
 """
 import os
 import sys
@@ -23,10 +23,11 @@ def main():
     from enterprise_warp_amd import synth
     case = sys.argv[1] if len(sys.argv) > 1 else "system"
     nmax = int(sys.argv[sys.argv.index("--max") + 1]) if "--max" in sys.argv else 12
+    off = int(sys.argv[sys.argv.index("--seed-offset") + 1]) if "--seed-offset" in sys.argv else 0
     cfg = (synth.config_system(os.path.join(ROOT, "tests", "golden", "ref_examples")) if case == "system"
            else synth.config_wide(True))
     pta = cfg.pta
-    X = synth.prior_draws(pta, cfg.B, cfg.theta_seed)
+    X = synth.prior_draws(pta, cfg.B, cfg.theta_seed + off)
     eng = pta.engine()
     route = pta.get_lnlikelihood_batch(X)
     out = {}
@@ -48,6 +49,9 @@ def main():
     print("dd    - ref     ", (out[29][sel] - ext) / s)
     print("fp64 fwd - ref  ", (out[27][sel] - ext) / s)
     print("enterprise - ref", (ent - ext) / s)
+    worse = np.abs(route[sel] - ext) > np.maximum(np.maximum(np.abs(ent - ext), np.abs(out[29][sel] - ext)), s)
+    print(f"route worse than both enterprise's order and all-double-double (and strict): {int(worse.sum())} "
+          f"of {len(sel)}", flush=True)
 
 
 if __name__ == "__main__":

@@ -42,6 +42,8 @@ def main():
     ap.add_argument("--modes", default="0,34")
     ap.add_argument("--rounds", type=int, default=5)
     ap.add_argument("--kinds", default="prior,near")
+    ap.add_argument("--seed-offset", type=int, default=0,
+                    help="added to the case's theta seed (fresh draws beyond the bench's own batch)")
     ap.add_argument("--contract", action="store_true",
                     help="time the contraction stage alone (ewh_contract_device) instead of the lnL batch")
     args = ap.parse_args()
@@ -55,8 +57,9 @@ def main():
         eng = pta.engine(0)
         U = len(pta.signal_collections) * B
         out = torch.zeros(B, dtype=torch.float64, device="cuda")
-        draws = {"prior": lambda: synth.prior_draws(pta, B, cfg.theta_seed),
-                 "near": lambda: synth.near_draws(pta, cfg.truth, B, cfg.theta_seed + 1)}
+        sd = cfg.theta_seed + args.seed_offset
+        draws = {"prior": lambda: synth.prior_draws(pta, B, sd),
+                 "near": lambda: synth.near_draws(pta, cfg.truth, B, sd + 1)}
         for kind in args.kinds.split(","):
             th = torch.from_numpy(draws[kind]()).cuda()
             times = {m: [] for m in modes}
