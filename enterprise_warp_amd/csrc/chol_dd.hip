@@ -92,15 +92,31 @@ struct DdLds {
 template <int PW>
 size_t dd_lds(int n) { return (size_t)(PW * n + PW * PW + PW + n) * sizeof(double2) + 8 * sizeof(double); }
 
+// 1 / sqrt(d) in double-double: the fp64 reciprocal square root and one
+// Newton step y + y (1 - d y^2) / 2 with d y^2 formed in double-double (the
+// step's own error ~ (3/8) e^2 with e ~ 1e-16).  Round 5 (r05j): replaces
+// dd_div(1, dd_sqrt(d)) -- one IEEE sqrt and three IEEE divisions in every
+// pivot of wave 0's serial chain
+__device__ __forceinline__ dd dd_rsqrt(dd d) {
+  const double y = rsqrt_fast(d.hi);
+  const double t = y * y, te = fma(y, y, -t);
+  const dd u = dd_mul(d, {t, te});
+  const double e = (1.0 - u.hi) - u.lo;
+  return dd_fast(y, y * (0.5 * e));
+}
+
 // Wave 0, lanes c < PW: factor the diagonal block DG (upper part valid) of
-// the panel starting at r0; pivots r0 + p < n - 1 add log d_p to ldet and
-// must be positive; the pivot n - 1 is q.  Leaves the strict upper part of
-// U_kk in DG and the scales 1/sqrt(d_p) in SC for the panel solve.
+// the panel starting at r0; pivots r0 + p < n - 1 add log d_p to ldet (lane
+// p's own term: the logs are taken after the chain, one per lane, and
+// summed over the wave at the end) and must be positive; the pivot n - 1 is
+// q.  Leaves the strict upper part of U_kk in DG and the scales 1/sqrt(d_p)
+// in SC for the panel solve.
 template <int PW>
 __device__ __forceinline__ void dd_factor_diag(const DdLds<PW>& S, int r0, int n, int lane, double& ldet, bool& ok, double& qv) {
   dd a[PW];
 #pragma unroll
   for (int r = 0; r < PW; ++r) a[r] = (lane < PW && r <= lane) ? ld2(S.DG[r * PW + lane]) : dd{0.0, 0.0};
+  double my_d = 1.0, my_c = 0.0;                     // lane p: d_p.hi and d_p.lo / d_p.hi
 #pragma unroll
   for (int p = 0; p < PW; ++p) {
     const dd d = readlane_dd(a[p], p);
@@ -110,8 +126,11 @@ __device__ __forceinline__ void dd_factor_diag(const DdLds<PW>& S, int r0, int n
       continue;
     }
     ok = ok && d.hi > 0.0;
-    ldet += log(d.hi) + d.lo / d.hi;
-    const dd s = dd_div({1.0, 0.0}, dd_sqrt(d));
+    const dd s = dd_rsqrt(d);
+    if (lane == p) {
+      my_d = d.hi;
+      my_c = d.lo * (s.hi * s.hi);
+    }
     if (lane == 0) S.SC[p] = st2(s);
     if (lane > p) a[p] = dd_mul(a[p], s);           // U[p][c], c > p
 #pragma unroll
@@ -124,6 +143,7 @@ __device__ __forceinline__ void dd_factor_diag(const DdLds<PW>& S, int r0, int n
 #pragma unroll
   for (int p = 0; p < PW; ++p)
     if (lane > p && lane < PW) S.DG[p * PW + lane] = st2(a[p]);
+  if (lane < PW) ldet += log(my_d) + my_c;           // (1, 0 for q and the lanes past PW)
   lds_wave_sync();
 }
 
@@ -314,6 +334,7 @@ __device__ __forceinline__ void chol_ddb_unit(const CholJob* __restrict__ jobs, 
     __threadfence_block();
     __syncthreads();
   }
+  if (wave == 0) ldet = wave_sum(ldet);              // (each lane holds its own pivots' logs)
   if (tid == 0) {
     double lnl = J.K[(long long)(b - b_off) * J.kstride] - 0.5 * qv - 0.5 * ldet - 0.5 * lphi;
     if (!ok || J.fail) lnl = -INFINITY;
