@@ -63,12 +63,16 @@ void chol_wide_kernel(const CholJob* __restrict__ jobs, int B, long long u0, int
   const CholJob J = jobs[p];
   const int LD = J.ld, NB = LD >> 4;
   const int nfact = NB - keep;
-  const gdptr A = (gdptr)(J.mats + (long long)(b - b_off) * J.mstride);
   // the reversed (verify) pass reads fl(hi + 2 lo) where the input is held
   // to double-double (S_lo / G_lo): the forward pass's input is X - lo, this
   // one's X + lo (to an ulp), so the two straddle the exact input and their
-  // difference also shows how much the input's own rounding moves the lnL
-  const gdptr Alo = (rev && J.mats_lo) ? (gdptr)(J.mats_lo + (long long)(b - b_off) * J.mstride) : nullptr;
+  // difference also shows how much the input's own rounding moves the lnL.
+  // Round 5 (r05j): a shared matrix's fl(hi + 2 lo) is formed once
+  // (mats_rev): the second load per element had cost the reversed pass 0.49
+  // -> 0.80 ms at the system model's 4096 units -- the same value, read once
+  const bool rv = rev && J.mats_rev;
+  const gdptr A = (gdptr)((rv ? J.mats_rev : J.mats) + (long long)(b - b_off) * J.mstride);
+  const gdptr Alo = (rev && !rv && J.mats_lo) ? (gdptr)(J.mats_lo + (long long)(b - b_off) * J.mstride) : nullptr;
   const double* th = theta + (long long)b * ldth;
   __attribute__((address_space(1))) double* scr =
       (__attribute__((address_space(1))) double*)(scratch + (long long)blockIdx.x * scr_per_wg + lane * 4);

@@ -281,6 +281,10 @@ struct CholJob {
   // the low part of a double-double matrix (chol_dd_kernel; same stride as
   // mats), or NULL
   const double* mats_lo = nullptr;
+  // the reversed verify pass's input fl(hi + 2 lo), formed once where the
+  // matrix is shared by every sample (mstride 0: the fixed-WN cache), or NULL
+  // (the pass then forms it from mats and mats_lo at every load)
+  const double* mats_rev = nullptr;
 };
 
 // one distinct spectrum of a fixed-WN job: phi = sum of its ne entries

@@ -1362,6 +1362,14 @@ __global__ void common_final_kernel(const double* __restrict__ ldet, const doubl
 }
 
 // out[b] = sum_p units[p * B + b], pulsars in order.
+// fl(hi + 2 lo) of a double-double matrix: the reversed verify pass's input
+// (chol_wide_kernel forms the same value per load where it is not cached)
+__global__ void rev_input_kernel(const double* __restrict__ hi, const double* __restrict__ lo, double* __restrict__ out,
+                                 long long n) {
+  const long long i = (long long)blockIdx.x * 256 + threadIdx.x;
+  if (i < n) out[i] = hi[i] + 2.0 * lo[i];
+}
+
 __global__ void reduce_units_kernel(const double* __restrict__ units, int P, int B, double* __restrict__ out) {
   const int b = blockIdx.x * blockDim.x + threadIdx.x;
   if (b >= B) return;
@@ -1433,6 +1441,7 @@ struct PsrHost {
   int* d_fx_urep = nullptr;       // fixed columns -> distinct-spectrum record (-1: no entry)
   double* d_S = nullptr;          // fx_ld^2
   double* d_Slo = nullptr;        // fx_ld^2, the low part of S (dd_path pulsars only)
+  double* d_Srev = nullptr;       // fx_ld^2, fl(S + 2 S_lo): the reversed verify pass's input (with d_Slo)
   bool has_theta_white = false;
   int n_slot = 0;
   ewh_pref* d_slots = nullptr;    // device copy of the white-noise slot table (PsrDev::slots)
@@ -2048,6 +2057,7 @@ int setup_fixed(DevCtx* h) {
     // the low part of S for the double-double factorisation (uncorrelated
     // bases past the register kernels, dd_path)
     if (!ps.d_Slo && dd_path(h, ps.fx_nb, true) && (rc = dalloc(h, &ps.d_Slo, (size_t)ps.fx_ld * ps.fx_ld))) return rc;
+    if (ps.d_Slo && !ps.d_Srev && (rc = dalloc(h, &ps.d_Srev, (size_t)ps.fx_ld * ps.fx_ld))) return rc;
     hipLaunchKernelGGL(schur_kernel, dim3(1), dim3(256), 0, h->stream, G, Glo, ps.ld, ps.m, ps.nlead, ps.d_colptr,
                        ps.d_spec, Kb_h, ps.d_S, ps.fx_ld, ps.nloc, ps.gstart, ps.ncommon, h->d_fxK + p,
                        h->d_fxfail + p, ps.d_Slo);
@@ -2059,6 +2069,13 @@ int setup_fixed(DevCtx* h) {
     jobs[p] = CholJob{ps.d_S, 0, ps.fx_ld, mreal, ps.d_fx_colptr, ps.d_fx_spec, h->d_fxK + p, 0, 0,
                       ps.d_fx_rep, ps.d_fx_ulist, ps.fx_nu, h->stage_spectra ? ps.d_fx_urec : nullptr, ps.d_fx_urep};
     jobs[p].mats_lo = ps.d_Slo;
+    if (ps.d_Slo) {          // the reversed verify pass's input, once (chol_wide.hip)
+      const long long ne = (long long)ps.fx_ld * ps.fx_ld;
+      hipLaunchKernelGGL(rev_input_kernel, dim3((unsigned)((ne + 255) / 256)), dim3(256), 0, h->stream, ps.d_S, ps.d_Slo,
+                         ps.d_Srev, ne);
+      EWH_HIP(hipGetLastError());
+      jobs[p].mats_rev = ps.d_Srev;
+    }
     if (jobs[p].urec != nullptr) {
       jobs[p].ntidx = (int)ps.fx_tidx.size();
       for (int i = 0; i < jobs[p].ntidx; ++i) jobs[p].tidx[i] = ps.fx_tidx[i];
