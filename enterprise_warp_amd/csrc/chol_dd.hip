@@ -80,17 +80,19 @@ struct DdLds {
   // dynamic LDS: U [PW][n] | DG [PW][PW] | SC [PW] | phinv [n] | red [8]
   double2 *U, *DG, *SC, *ph;
   double* red;
+  int* ctr;                  // the trailing update's tile counter
   __device__ DdLds(double2* base, int n) {
     U = base;
     DG = U + PW * n;
     SC = DG + PW * PW;
     ph = SC + PW;
     red = (double*)(ph + n);
+    ctr = (int*)(red + 8);
   }
 };
 
 template <int PW>
-size_t dd_lds(int n) { return (size_t)(PW * n + PW * PW + PW + n) * sizeof(double2) + 8 * sizeof(double); }
+size_t dd_lds(int n) { return (size_t)(PW * n + PW * PW + PW + n) * sizeof(double2) + 8 * sizeof(double) + 16; }
 
 // 1 / sqrt(d) in double-double: the fp64 reciprocal square root and one
 // Newton step y + y (1 - d y^2) / 2 with d y^2 formed in double-double (the
@@ -162,6 +164,7 @@ __device__ __forceinline__ void chol_ddb_unit(const CholJob* __restrict__ jobs, 
   // trailing update, bit 1 the panel solve, bit 2 wave 0's diagonal chain;
   // the results are then meaningless.  0 in the product)
   const int tid = threadIdx.x, wave = tid >> 6, lane = tid & 63;
+  constexpr bool RSOLVE_STATIC = !RSOLVE;          // (dev mode 34: the r05a tile dealing too)
   // (uniform: the job's fields load into scalar registers, not 50 VGPRs)
   const int p_ = __builtin_amdgcn_readfirstlane((int)(u / B)), b = __builtin_amdgcn_readfirstlane((int)(u % B));
   const CholJob& J = jobs[p_];
@@ -212,6 +215,7 @@ __device__ __forceinline__ void chol_ddb_unit(const CholJob* __restrict__ jobs, 
   for (int r0 = 0; r0 + PW < n; r0 += PW) {
     const bool first = r0 == 0;
     const int t0 = r0 + PW, m = n - t0;
+    if (tid == 0 && !RSOLVE_STATIC) *S.ctr = 0;      // (phase B's tile counter; nothing reads it in A)
     // A. panel solve by forward substitution, one thread per column j:
     // U[p][j] = s_p (A[r0 + p][j] - sum_{r < p} U_kk[r][p] U[r][j])
     for (int jj = tid; jj < ((dbg & 2) ? 0 : m); jj += DD_THREADS) {
@@ -284,13 +288,30 @@ __device__ __forceinline__ void chol_ddb_unit(const CholJob* __restrict__ jobs, 
       }
       lds_wave_sync();
       if (!(dbg & 4)) dd_factor_diag<PW>(S, t0, n, lane, ldet, ok, qv);
-    } else {
+    }
+    // the rest of the trailing update, 64 tiles per grab from an LDS counter
+    // (r05j; wave 0 joins after its chain -- the tiles were dealt to waves
+    // 1-7 by a fixed stride before): per tile the same operations
+    if (RSOLVE_STATIC ? wave != 0 : true) {
       constexpr int QD = PW / 4;                 // 4x4 tiles inside the next diagonal block
-      const int ntiles = T * (T + 1) / 2;
-      for (int idx = tid - 64; idx < ((dbg & 1) ? 0 : ntiles); idx += DD_THREADS - 64) {
-        int ti, tj;
-        tri_decode(T, idx, ti, tj);
-        if (tj < QD) continue;                   // (wave 0's)
+      const int ntiles = (dbg & 1) ? 0 : T * (T + 1) / 2;
+      for (int gi = 0;; ++gi) {
+        int idx;
+        if constexpr (RSOLVE_STATIC) {
+          idx = tid - 64 + gi * (DD_THREADS - 64);
+          if (idx >= ntiles) break;
+        } else {
+          // (every lane of the wave is active here: one grab per wave, the
+          // base broadcast from the lane that made it)
+          int base = 0;
+          if (lane == 0) base = atomicAdd(S.ctr, 64);
+          base = __shfl(base, 0);
+          if (base >= ntiles) break;
+          idx = base + lane;
+        }
+        int ti = 0, tj = 0;
+        if (idx < ntiles) tri_decode(T, idx, ti, tj);
+        if (idx < ntiles && tj >= QD) {          // (tj < QD: wave 0's)
         const int i0 = t0 + 4 * ti, j0 = t0 + 4 * tj;
         double ah[4][4], al[4][4];
 #pragma unroll
@@ -329,6 +350,7 @@ __device__ __forceinline__ void chol_ddb_unit(const CholJob* __restrict__ jobs, 
             H[o] = v.hi;
             L[o] = v.lo;
           }
+        }
       }
     }
     __threadfence_block();
