@@ -368,6 +368,58 @@ CPU_JSON_ENV = "EWARP_BENCH_CPU_JSON"   # launcher -> rank 0: the CPU baseline i
 LAUNCHER_ENV = "EWARP_BENCH_LAUNCHER"   # set in the ranks bench.py itself starts
 
 
+def verify_default(flag, world):
+    """--verify / --no-verify as given; by default on exactly when the run has
+    more than one rank (the driver runs plain `bench.py --gpus N`: a
+    multi-rank line must carry its own correctness evidence)."""
+    return (world > 1) if flag is None else bool(flag)
+
+
+def device_identity(index):
+    """PCI bus id and UUID of device `index` of this process (hipDeviceGetPCIBusId
+    through the HIP runtime torch loaded; torch's device properties)."""
+    import ctypes
+    import torch
+    ident = {"index": int(index), "pci_bus_id": None, "uuid": None}
+    try:
+        ident["uuid"] = str(torch.cuda.get_device_properties(index).uuid)
+    except Exception:  # noqa: BLE001
+        pass
+    hip = None
+    try:   # the runtime already mapped into this process (never a second copy)
+        with open("/proc/self/maps") as fh:
+            paths = sorted({ln.split()[-1] for ln in fh if "libamdhip64.so" in ln})
+        if paths:
+            hip = ctypes.CDLL(paths[0], mode=os.RTLD_NOLOAD | ctypes.RTLD_GLOBAL)
+    except OSError:
+        hip = None
+    if hip is not None:
+        buf = ctypes.create_string_buffer(64)
+        if hip.hipDeviceGetPCIBusId(buf, 64, int(index)) == 0:
+            ident["pci_bus_id"] = buf.value.decode()
+    return ident
+
+
+def run_problems(devices, same_device, verify, verify_on):
+    """What makes a bench line invalid (rank 0 exits non-zero on any): two
+    ranks on one device without --same-device, a missing or failed verify
+    block where it was asked for (the reduced lnL against the single-device
+    entry: max error > strict, or a different -inf pattern)."""
+    out = []
+    keys = [d.get("pci_bus_id") or d.get("uuid") or f"index{d.get('index')}" for d in devices]
+    if len(devices) > 1 and not same_device and len(set(keys)) < len(keys):
+        out.append(f"ranks share a device without --same-device: {keys}")
+    if verify_on:
+        if verify is None:
+            out.append("verify requested but not run")
+        else:
+            if not verify["max_err_over_strict"] <= 1.0:
+                out.append(f"verify: max error {verify['max_err_over_strict']:.3e} x strict")
+            if not verify["inf_pattern_equal"]:
+                out.append("verify: -inf pattern differs from the single-device entry")
+    return out
+
+
 def free_port():
     with socket.socket() as s:
         s.bind(("127.0.0.1", 0))
@@ -481,12 +533,16 @@ def main():
                     help="nccl (= RCCL, the default); gloo only to rehearse the multi-rank path")
     ap.add_argument("--same-device", action="store_true",
                     help="every rank on cuda:0 (rehearsal on a one-GPU box; needs --dist-backend gloo)")
-    ap.add_argument("--verify", action="store_true",
-                    help="rank 0 checks the reduced lnL of the first samples against the single-device entry")
+    ap.add_argument("--verify", dest="verify", action="store_true", default=None,
+                    help="rank 0 checks the reduced lnL of the first samples against the single-device entry "
+                         "(default with more than one rank; DESIGN.md §5)")
+    ap.add_argument("--no-verify", dest="verify", action="store_false",
+                    help="skip that check (a multi-rank line then carries no correctness evidence)")
     args = ap.parse_args()
     if args.same_device and args.dist_backend != "gloo":
         ap.error("--same-device needs --dist-backend gloo (RCCL takes one rank per GPU)")
     world, spawn = resolve_world(args.gpus, os.environ)
+    args.verify = verify_default(args.verify, world)
     if spawn:
         # launcher: the CPU baseline on this job's cores first, then the ranks
         cpu = None
@@ -531,6 +587,11 @@ def main():
     rccl_world = dist.get_world_size() if world > 1 else 1
     if rccl_world != world:
         raise SystemExit(f"bench.py: the process group has {rccl_world} ranks, --gpus / WORLD_SIZE say {world}")
+    # every rank's device identity (PCI bus id / UUID), gathered to all
+    devices = [device_identity(gpu)]
+    if world > 1:
+        devices = [None] * world
+        dist.all_gather_object(devices, device_identity(gpu))
 
     cfg = synth.config_c3()
     pta = cfg.pta
@@ -606,7 +667,7 @@ def main():
     per_rank = t.cpu().numpy().reshape(world, 2)
     elapsed = float(per_rank[:, 0].max())
     lnl = outs[(args.steps - 1) & 1].cpu().numpy()
-    verify = None
+    verify, problems = None, []
     if args.verify and rank == 0:
         # the reduced batch against the single-device entry (ewh_lnl_batch,
         # pulsar-order device fold) on its first samples: strict bound
@@ -664,6 +725,7 @@ def main():
                        "finite_fraction": float(np.mean(np.isfinite(lnl)))},
             "rccl_world": rccl_world,
             "dist": {"backend": args.dist_backend if world > 1 else None, "same_device": bool(args.same_device),
+                     "devices": devices,
                      "launcher": "bench.py" if os.environ.get(LAUNCHER_ENV) else
                      ("torchrun" if os.environ.get("TORCHELASTIC_RUN_ID") else None),
                      "partition": args.c3_partition,
@@ -688,9 +750,16 @@ def main():
             rec["sampler_latency"] = latency
         if verify is not None:
             rec["verify"] = verify
+        problems = run_problems(devices, args.same_device, verify, args.verify)
+        if problems:
+            rec["problems"] = problems
         print(json.dumps(rec), flush=True)
+        if problems:
+            print("bench.py: " + "; ".join(problems), file=sys.stderr, flush=True)
     if world > 1:
         dist.destroy_process_group()
+    if rank == 0 and problems:
+        sys.exit(3)
 
 
 def main_c5(args):

@@ -21,7 +21,7 @@ LIB_PATH = os.environ.get("EWARP_HIP_LIB") or (CPU_LIB_PATH if BACKEND == "cpu" 
                                                os.path.join(_HERE, "libewarp_hip.so"))
 DEV_LIB_PATH = os.path.join(_HERE, "libewarp_hip_dev.so")
 
-EWH_ABI_VERSION = 6
+EWH_ABI_VERSION = 7
 COMMON_CORRELATED, COMMON_OPTSTAT = 0, 1
 SPEC_POWERLAW, SPEC_TURNOVER, SPEC_FREESPEC, SPEC_CONST = 1, 2, 3, 4
 
@@ -91,6 +91,12 @@ def load():
         raise EngineError(f"{LIB_PATH} not built: run `make -C enterprise_warp_amd/csrc` or "
                           "__graft_entry__.build(); there is no CPU fallback")
     lib = C.CDLL(LIB_PATH)
+    # a library of an older ABI lacks entry points: say so before typing them
+    missing = [n for n in EXPORTS if not hasattr(lib, n)]
+    if missing or lib.ewh_version() != EWH_ABI_VERSION:
+        raise EngineError(f"{LIB_PATH}: library out of date (ABI version mismatch"
+                          f"{'; missing ' + ', '.join(missing) if missing else ''}); rebuild it "
+                          "(make -C enterprise_warp_amd/csrc)")
     lib.ewh_create.argtypes = [C.POINTER(PtaDesc), _ip, C.c_int32, C.POINTER(C.c_void_p)]
     lib.ewh_create.restype = C.c_int
     lib.ewh_num_devices.argtypes = [C.c_void_p]
@@ -137,8 +143,6 @@ def load():
         lib.ewh_dev_gram.restype = C.c_int
         lib.ewh_dev_reduced.argtypes = [C.c_void_p, C.c_int32, _dp, _dp]
         lib.ewh_dev_reduced.restype = C.c_int
-    if lib.ewh_version() != EWH_ABI_VERSION:
-        raise EngineError("libewarp_hip.so ABI version mismatch")
     _lib = lib
     return lib
 

@@ -37,6 +37,10 @@
 
 #include <cstdlib>
 
+// every function below: error-free transformations -- no contraction of a
+// product into a later sum (ewarp_dev.h, the double-double helpers)
+#pragma clang fp contract(off)
+
 namespace ewh_dev {
 namespace {
 
@@ -175,6 +179,7 @@ __device__ __forceinline__ void chol_ddb_unit(const CholJob* __restrict__ jobs, 
   const double* Slo = J.mats_lo ? J.mats_lo + moff : nullptr;
   double* H = scratch + (long long)blockIdx.x * scr_per_wg;
   double* L = H + (long long)n * n;
+  EWH_DCHECK(2LL * n * n <= scr_per_wg && n % 16 == 0 && n >= PW, "chol_dd scratch slot holds the unit");
   // phi^-1 per column in double-double (pads and r carry no entry: 0)
   double lphi = 0.0;
   for (int a = tid; a < n; a += DD_THREADS) {
@@ -220,6 +225,7 @@ __device__ __forceinline__ void chol_ddb_unit(const CholJob* __restrict__ jobs, 
     // U[p][j] = s_p (A[r0 + p][j] - sum_{r < p} U_kk[r][p] U[r][j])
     for (int jj = tid; jj < ((dbg & 2) ? 0 : m); jj += DD_THREADS) {
       const int j = t0 + jj;
+      EWH_DCHECK(j < n && (long long)(r0 + PW - 1) * n + j < (long long)n * n, "chol_dd panel solve: column in range");
       dd a[PW];
 #pragma unroll
       for (int r = 0; r < PW; ++r) {
@@ -303,6 +309,8 @@ __device__ __forceinline__ void chol_ddb_unit(const CholJob* __restrict__ jobs, 
         } else {
           // (every lane of the wave is active here: one grab per wave, the
           // base broadcast from the lane that made it)
+          EWH_DCHECK(__builtin_amdgcn_read_exec() == ~0ull, "chol_dd tile grab: every lane active");
+          EWH_DCHECK(gi <= ntiles / 64 + 1, "chol_dd tile grab: iteration bound");
           int base = 0;
           if (lane == 0) base = atomicAdd(S.ctr, 64);
           base = __shfl(base, 0);
@@ -313,6 +321,7 @@ __device__ __forceinline__ void chol_ddb_unit(const CholJob* __restrict__ jobs, 
         if (idx < ntiles) tri_decode(T, idx, ti, tj);
         if (idx < ntiles && tj >= QD) {          // (tj < QD: wave 0's)
         const int i0 = t0 + 4 * ti, j0 = t0 + 4 * tj;
+        EWH_DCHECK(ti <= tj && j0 + 3 < n && i0 >= t0, "chol_dd trailing tile inside the trailing triangle");
         double ah[4][4], al[4][4];
 #pragma unroll
         for (int x = 0; x < 4; ++x)
@@ -378,6 +387,7 @@ __global__ __launch_bounds__(DD_THREADS) void chol_dd_kernel(const CholJob* __re
   extern __shared__ __attribute__((aligned(16))) double2 dd_smem[];
   // one call site (the unit body is inlined once)
   const int cnt = list ? *count : (int)gridDim.x;
+  EWH_DCHECK(!list || cnt >= 0, "chol_dd list count");
   for (int i = blockIdx.x; i < cnt; i += gridDim.x) {
     const long long u = list ? (long long)list[i] : u0 + i;
     chol_ddb_unit<PW, RSOLVE>(jobs, B, u, b_off, theta + (long long)(u % B) * ldth, out_units, scratch, scr_per_wg,
@@ -399,17 +409,30 @@ constexpr double VERIFY_FRAC = 0.0625;
 __global__ __launch_bounds__(256) void verify_units_kernel(const double* __restrict__ a, const double* __restrict__ b,
                                                            long long u0, long long n, double frac,
                                                            int* __restrict__ list, int* __restrict__ count,
-                                                           int* __restrict__ total) {
+                                                           unsigned long long* __restrict__ total) {
   const long long i = (long long)blockIdx.x * 256 + threadIdx.x;
-  if (total && i == 0) atomicAdd(total + 1, (int)n);     // (ewh_refine_stats: units checked)
+  if (total && i == 0) atomicAdd(total + 1, (unsigned long long)n);     // (ewh_refine_stats: units checked)
   if (i >= n) return;
   const long long u = u0 + i;
   const double x = a[u], y = b[u];
   const bool fx = x - x == 0.0, fy = y - y == 0.0;           // finite
-  const bool bad = (fx != fy) || (fx && fabs(x - y) > frac * (1e-6 + 1e-10 * fabs(x)));
+  // (round 6: a non-finite term of either order is refactored too -- the two
+  // agreeing on -inf is a rounding failure of both wherever the exact Sigma
+  // is positive definite; with a == b this is the failure scan of
+  // refine_failed)
+  const bool bad = frac < 0.0 || !fx || !fy || fabs(x - y) > frac * (1e-6 + 1e-10 * fabs(x));
   if (bad) {
-    list[atomicAdd(count, 1)] = (int)u;
-    if (total) atomicAdd(total, 1);       // (ewh_refine_stats: units refined)
+    const int slot = atomicAdd(count, 1);
+    EWH_DCHECK(slot < n, "verify list slot within the units checked");
+    list[slot] = (int)u;
+    if (total) atomicAdd(total, 1ull);    // (ewh_refine_stats: units refined)
+  }
+}
+
+__global__ void count_units_kernel(unsigned long long* __restrict__ total, long long n) {
+  if (threadIdx.x == 0) {
+    atomicAdd(total, (unsigned long long)n);
+    atomicAdd(total + 1, (unsigned long long)n);
   }
 }
 
@@ -458,10 +481,17 @@ int set_dd_attributes() {
   return 0;
 }
 
-int launch_verify_units(const double* a, const double* b, long long u0, long long n, int* list, int* count,
-                        int* total, hipStream_t st) {
+int launch_count_units(unsigned long long* total, long long n, hipStream_t st) {
   if (n <= 0) return 0;
-  double frac = VERIFY_FRAC;
+  hipLaunchKernelGGL(count_units_kernel, dim3(1), dim3(64), 0, st, total, n);
+  const hipError_t e = hipGetLastError();
+  return e == hipSuccess ? 0 : set_err(EWH_E_HIP, std::string("count_units_kernel: ") + hipGetErrorString(e));
+}
+
+int launch_verify_units(const double* a, const double* b, long long u0, long long n, int* list, int* count,
+                        unsigned long long* total, hipStream_t st, bool all) {
+  if (n <= 0) return 0;
+  double frac = all ? -1.0 : VERIFY_FRAC;
 #ifdef EWH_DEV
   if (const char* e = getenv("EWARP_VERIFY_FRAC")) frac = atof(e);   // (dev calibration only)
 #endif

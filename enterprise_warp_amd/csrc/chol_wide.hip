@@ -63,6 +63,12 @@ void chol_wide_kernel(const CholJob* __restrict__ jobs, int B, long long u0, int
   const CholJob J = jobs[p];
   const int LD = J.ld, NB = LD >> 4;
   const int nfact = NB - keep;
+  // (debug build: the unit's packed U blocks fit its scratch slot, the
+  // phi^-1 table its LDS array, the unit lies inside the batch)
+  EWH_DCHECK(LD <= WIDE_LD_MAX && LD % 16 == 0 && keep >= 0 && keep < NB, "chol_wide: width within WIDE_LD_MAX");
+  EWH_DCHECK([&] { long long sz = 0; for (int pp = 0; pp < nfact; ++pp) sz += NB - pp; return sz * 256; }() <=
+                 scr_per_wg, "chol_wide: U blocks fit the scratch slot");
+  EWH_DCHECK(b >= b_off && p >= 0, "chol_wide: unit inside the batch");
   // the reversed (verify) pass reads fl(hi + 2 lo) where the input is held
   // to double-double (S_lo / G_lo): the forward pass's input is X - lo, this
   // one's X + lo (to an ulp), so the two straddle the exact input and their

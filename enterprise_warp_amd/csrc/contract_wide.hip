@@ -312,6 +312,9 @@ __global__ __launch_bounds__(256) void contract_xr_kernel(PsrDev P, const double
   // (its w rows) and stream the same T rows through that XCD's L2
   const long long L = xcd_unit(blockIdx.x, gridDim.x);
   const int sg = (int)(L / npair), pr = (int)(L % npair);
+  // (debug build: the sample group and the block pair inside the launch)
+  EWH_DCHECK(sg * XR_S < nsamp && NB <= WIDE_NB_MAX && (long long)nsamp * P.n_toa * 8 < (1LL << 32),
+             "contract_xr: sample group / 32-bit weight offsets in range");
   int bi = 0, rem = pr;
   while (rem >= NB - bi) {
     rem -= NB - bi;

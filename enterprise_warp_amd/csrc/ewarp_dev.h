@@ -32,6 +32,29 @@ int set_err(int code, const std::string& msg);
       return ::ewh_dev::set_err(EWH_E_HIP, std::string(#expr) + ": " + hipGetErrorString(e_)); \
   } while (0)
 
+// Device-side invariant checks of the debug build (`make debug`: -DEWH_DEBUG,
+// build/libewarp_hip_debug.so; SURVEY.md §5's sanitizer row for device code).
+// A violated check prints its site, block and thread, then traps -- a bounded
+// failure with a location instead of a hang or a silent out-of-bounds access.
+// Sites: every work-grab / spin loop carries an iteration bound (and the
+// grab a full exec mask), and LDS / scratch / operand indices are checked
+// against their allocations in chol_dd, chol_wide and contract_xr.  The
+// product and dev builds compile the checks away.
+#ifdef EWH_DEBUG
+#define EWH_DCHECK(cond, what)                                                                           \
+  do {                                                                                                   \
+    if (!(cond)) {                                                                                       \
+      printf("EWH_DCHECK failed: %s (%s:%d) block %d,%d thread %d\n", what, __FILE__, __LINE__,          \
+             (int)blockIdx.x, (int)blockIdx.y, (int)threadIdx.x);                                        \
+      __builtin_trap();                                                                                  \
+    }                                                                                                    \
+  } while (0)
+#else
+#define EWH_DCHECK(cond, what) \
+  do {                         \
+  } while (0)
+#endif
+
 constexpr int MFMA_NB_MAX = 9;
 constexpr int CONTRACT2_NB_MAX = 13;
 constexpr int default_waves(int nb) { return nb <= 8 ? 2 : 1; }
@@ -193,33 +216,57 @@ static __device__ double block_sum256(double v, double* scratch) {
 
 // ----------------------------------------------------------------------------
 // double-double helpers (Knuth TwoSum, TwoProd by fma; Dekker / Bailey
-// normalisation): value = hi + lo with |lo| <= ulp(hi) / 2
+// normalisation): value = hi + lo with |lo| <= ulp(hi) / 2.
+// Every error-free transformation is compiled with floating-point
+// contraction off (`#pragma clang fp contract(off)`, round 6): hipcc's device
+// default (-ffp-contract=fast) fused `s = hi + x * y` into one fma while the
+// TwoSum error term still used the separately rounded product, which left
+// every "double-double" kernel (gram_dd, schur, chol_dd) only about fp64-
+// accurate -- the ~15x strict floor of the device's double-double twin
+// against the CPU double-double reference on C3 prior draws, and indefinite
+// C4 refinements (ISA: v_fma_f64 in place of v_add_f64)
 // ----------------------------------------------------------------------------
 struct dd {
   double hi, lo;
 };
 __device__ __forceinline__ dd dd_two_sum(double a, double b) {
+#pragma clang fp contract(off)
   const double s = a + b, bp = s - a;
   return {s, (a - (s - bp)) + (b - bp)};
 }
 __device__ __forceinline__ dd dd_fast(double a, double b) {   // |a| >= |b|
+#pragma clang fp contract(off)
   const double s = a + b;
   return {s, b - (s - a)};
 }
 __device__ __forceinline__ dd dd_add(dd x, dd y) {
+#pragma clang fp contract(off)
   const dd s = dd_two_sum(x.hi, y.hi);
   return dd_fast(s.hi, s.lo + x.lo + y.lo);
 }
+// x + y with both parts TwoSum-ed (the accurate double-double sum: a
+// relative error of ~2^-106 of |x + y| even under cancellation, which the
+// sloppy dd_add above does not bound)
+__device__ __forceinline__ dd dd_add_ieee(dd x, dd y) {
+#pragma clang fp contract(off)
+  dd s = dd_two_sum(x.hi, y.hi);
+  const dd t = dd_two_sum(x.lo, y.lo);
+  s = dd_fast(s.hi, s.lo + t.hi);
+  return dd_fast(s.hi, s.lo + t.lo);
+}
 __device__ __forceinline__ dd dd_mul(dd x, dd y) {
+#pragma clang fp contract(off)
   const double p = x.hi * y.hi;
   return dd_fast(p, fma(x.hi, y.hi, -p) + (x.hi * y.lo + x.lo * y.hi));
 }
 __device__ __forceinline__ dd dd_div(dd x, dd y) {          // one Newton correction of x.hi / y.hi
+#pragma clang fp contract(off)
   const double q = x.hi / y.hi;
   const dd r = dd_add(x, dd_mul({-q, 0.0}, y));
   return dd_fast(q, r.hi / y.hi);
 }
 __device__ __forceinline__ dd dd_sqrt(dd x) {
+#pragma clang fp contract(off)
   const double r = sqrt(x.hi);
   const dd e = dd_add(x, dd_mul({-r, 0.0}, {r, 0.0}));
   return dd_fast(r, e.hi / (2.0 * r));
@@ -1577,11 +1624,15 @@ int launch_chol_dd(const CholJob* jobs, int B, long long u0, long long n, int b_
 int set_dd_attributes();
 // the verify-and-refine form: units a (forward fp64) vs b (reversed fp64) of
 // [u0, u0 + n) -> list / count of the disagreeing ones (count zeroed by the
-// caller; total, if not NULL: total[0] += the count, total[1] += n), then
+// caller; total, if not NULL: total[0] += the count, total[1] += n; all:
+// every unit listed -- kernel mode 29's refine_failed), then
 // chol_dd_kernel over the list (cap workgroups looping) into units; r05a: the
 // round-5a panel solve (row-oriented; dev mode 34)
 int launch_verify_units(const double* a, const double* b, long long u0, long long n, int* list, int* count,
-                        int* total, hipStream_t st);
+                        unsigned long long* total, hipStream_t st, bool all = false);
+// kernel mode 29 (every unit in double-double): total[0] and total[1] += n on
+// the device, in stream order (so graph replays count, captures do not)
+int launch_count_units(unsigned long long* total, long long n, hipStream_t st);
 int launch_chol_dd_list(const CholJob* jobs, int B, int b_off, const double* theta, int ldth, double* units,
                         double* scr, long long scr_per_wg, long long cap, const int* list, const int* count, int ld,
                         hipStream_t st, bool r05a = false);

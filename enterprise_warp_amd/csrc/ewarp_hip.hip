@@ -157,68 +157,154 @@ __global__ __launch_bounds__(256) void epoch_sums_multi_kernel(PsrDev P, const d
 }
 
 // ----------------------------------------------------------------------------
-// fixed white noise, one-off (ewh_create / ewh_set_fixed_white): the cached
-// Gram G = T_aug^T W T_aug - sum_e beta_e s_e s_e^T with every entry summed
-// in double-double (Dot2, Ogita-Rump-Oishi 2005: TwoProd by fma, TwoSum) and
-// kept as hi + lo for the double-double timing-model elimination
-// (schur_kernel).  The products are exact: w T_a is itself split by TwoProd,
-// so each term is w_t T_ta T_tb with only w_t = 1/N_t rounded once (a
-// relative perturbation of N_t by <= 2^-53); the epoch sums s_e are fp64
-// (<= 16-32 TOAs each).  One fp64 MFMA accumulator over 20k TOAs moved
-// prior-draw lnL by up to 7e-2 on C3 through the ill-conditioned
-// timing-model elimination (tests/test_gpu_parity.py::
-// test_c3_bench_workload_prior_draws).  One workgroup per upper 16x16 block,
-// thread (ty, tx) -> entry (16 bi + ty, 16 bj + tx); 32-row TOA chunks staged
-// in LDS.  (Chromatic `vary` bases never take this path: their basis is
-// theta-dependent, so white noise is not cached.)
-__global__ __launch_bounds__(256) void gram_dd_kernel(PsrDev P, const double* __restrict__ w,
-                                                      const double* __restrict__ beta,
-                                                      const double* __restrict__ s, double* __restrict__ G,
-                                                      double* __restrict__ Glo) {
-  const int LD = P.ld, nb = P.nb;
-  int blk = blockIdx.x, bi = 0;
-  while (blk >= nb - bi) { blk -= nb - bi; ++bi; }
-  const int bj = bi + blk;
+// The double-double Gram G = X^T W X - sum_e beta_e s_e s_e^T of one pulsar,
+// X = T_aug = X_hi + X_lo: X_hi the projected basis the fp64 kernels read
+// (P.T), X_lo its projection residual (PsrHost::d_Tlo, round 6: X_hi + X_lo =
+// T - M C to double-double, create_ctx), so the Gram is that of the exactly
+// projected basis -- an exact reparametrisation of enterprise's -- and the
+// projection's fp64 rounding (a basis perturbation of O(eps |M C|), up to
+// ~1e-14 of the projected column's own size) stays out.  Every w_t X_ta X_tb
+// is summed in double-double (Dot2, Ogita-Rump-Oishi 2005: TwoProd by fma,
+// TwoSum): w X_a,hi is itself split by TwoProd, so each hi x hi term is exact
+// with only w_t = 1/N_t rounded once (a relative perturbation of N_t by <=
+// 2^-53, benign: it keeps G a Gram); the cross terms w (X_a,hi X_b,lo +
+// X_a,lo X_b,hi) are added to the low part in fp64.  The ECORR epoch sums
+// s_e = sum over the epoch of w_t (X_hi + X_lo)_t are formed here in fp64
+// (<= 16-32 TOAs).  Rounds 2-5 summed the Gram of the rounded projected basis:
+// on ill-conditioned prior draws that left the device's double-double twin
+// ~16x strict from the CPU double-double value on C3 and made C4 units
+// indefinite (tests/test_gpu_parity.py::test_headline_matches_dd_at_scale,
+// test_c4_bench_inf_sets_at_scale).  One workgroup per upper 16x16 block,
+// thread (ty, tx) -> entry (16 bi + ty, 16 bj + tx); 32-row chunks staged in
+// LDS.  Writes G_hi / G_lo of block (bi, bj) (both triangles).
+__device__ __forceinline__ void gram_dd_block(const PsrDev& P, const double* __restrict__ Xlo,
+                                              const double* __restrict__ w, const double* __restrict__ beta, int bi,
+                                              int bj, double* __restrict__ G, double* __restrict__ Glo,
+                                              double (*Ta)[17], double (*Tb)[17], double (*Ua)[17], double (*Ub)[17],
+                                              double* wv) {
+#pragma clang fp contract(off)
+  const int LD = P.ld;
   const int tx = threadIdx.x & 15, ty = threadIdx.x >> 4;
-  __shared__ double Ta[32][17], Tb[32][17], wv[32];
-  double hi = 0.0, lo = 0.0;
+  dd acc = {0.0, 0.0};
   for (int pass = 0; pass < 2; ++pass) {     // TOA rows (w), then epoch rows (-beta)
     const int nrows = pass == 0 ? P.n_toa : P.n_epoch;
-    const double* src = pass == 0 ? P.T : s;
-    const double* ws = pass == 0 ? w : beta;
-    const double sg = pass == 0 ? 1.0 : -1.0;
     for (int t0 = 0; t0 < nrows; t0 += 32) {
-      for (int idx = threadIdx.x; idx < 512; idx += 256) {
-        const int r = idx >> 4, cc = idx & 15;
-        const bool in = t0 + r < nrows;
-        Ta[r][cc] = in ? src[(long long)(t0 + r) * LD + 16 * bi + cc] : 0.0;
-        Tb[r][cc] = in ? src[(long long)(t0 + r) * LD + 16 * bj + cc] : 0.0;
+      for (int idx = threadIdx.x; idx < 1024; idx += 256) {
+        const int r = idx >> 5, c = idx & 31, cc = c & 15;
+        const int col = 16 * (c < 16 ? bi : bj) + cc;
+        double v = 0.0, vl = 0.0;
+        if (t0 + r < nrows) {
+          if (pass == 0) {
+            const long long o = (long long)(t0 + r) * LD + col;
+            v = P.T[o];
+            vl = Xlo ? Xlo[o] : 0.0;
+          } else {
+            // s_e[col] = sum over the epoch's rows of w_t X_t,col in
+            // double-double (round 6; fp64 until then -- a relative rounding
+            // of the rank-one ECORR term, i.e. of G itself)
+            for (int t = P.ep_start[t0 + r]; t < P.ep_stop[t0 + r]; ++t) {
+              const long long o = (long long)t * LD + col;
+              const double p = w[t] * P.T[o];
+              const double pe = fma(w[t], P.T[o], -p);
+              const double sum = v + p, bp = sum - v;
+              vl += ((v - (sum - bp)) + (p - bp)) + pe + (Xlo ? w[t] * Xlo[o] : 0.0);
+              v = sum;
+            }
+          }
+        }
+        if (c < 16) {
+          Ta[r][cc] = v;
+          Ua[r][cc] = vl;
+        } else {
+          Tb[r][cc] = v;
+          Ub[r][cc] = vl;
+        }
       }
-      if (threadIdx.x < 32) wv[threadIdx.x] = t0 + (int)threadIdx.x < nrows ? sg * ws[t0 + threadIdx.x] : 0.0;
+      if (threadIdx.x < 32)
+        wv[threadIdx.x] = t0 + (int)threadIdx.x < nrows ? (pass == 0 ? w[t0 + threadIdx.x] : -beta[t0 + threadIdx.x])
+                                                        : 0.0;
       __syncthreads();
+      // the tile's 32 terms by Dot2 into a fresh (hi, lo), then added to the
+      // running total in double-double (round 6: one Dot2 over all rows had an
+      // error bound of gamma_n^2 sum |terms| -- ~5e-24 of it at 20k TOAs; now
+      // gamma_32^2 per tile and 2^-106 per tile fold)
+      double hi = 0.0, lo = 0.0;
       for (int r = 0; r < 32; ++r) {
-        const double wa = wv[r], ta = Ta[r][ty], y = Tb[r][tx];
+        const double wa = wv[r], ta = Ta[r][ty], yv = Tb[r][tx];
         const double x = wa * ta;
-        const double xe = fma(wa, ta, -x);          // TwoProd: w T_a = x + xe exactly
-        const double p = x * y;
-        const double pe = fma(x, y, -p);            // TwoProd: x y = p + pe exactly
-        const double sum = hi + p;                  // TwoSum: hi + p = sum + se exactly
+        const double xe = fma(wa, ta, -x);          // TwoProd: w X_a = x + xe exactly
+        const double pr = x * yv;
+        const double pe = fma(x, yv, -pr);          // TwoProd: x X_b = pr + pe exactly
+        const double sum = hi + pr;                 // TwoSum: hi + pr = sum + se exactly
         const double bp = sum - hi;
-        const double se = (hi - (sum - bp)) + (p - bp);
+        const double se = (hi - (sum - bp)) + (pr - bp);
         hi = sum;
-        lo += se + fma(xe, y, pe);
+        // + the low parts' cross terms (X_lo, or the epoch sums' low parts)
+        lo += se + fma(xe, yv, pe) + wa * fma(ta, Ub[r][tx], Ua[r][ty] * yv);
       }
+      acc = dd_add_ieee(acc, dd_two_sum(hi, lo));
       __syncthreads();
     }
   }
   const int row = 16 * bi + ty, col = 16 * bj + tx;
   if (row > col) return;      // diagonal block: the upper entry's thread writes both (exactly symmetric)
-  dd v = dd_fast(hi, lo);
+  dd v = acc;
   if (row == col && row >= P.m && row < LD - 1) v = {1.0, 0.0};   // unit pads, as the contraction kernels
   G[(long long)row * LD + col] = v.hi;
   G[(long long)col * LD + row] = v.hi;
   Glo[(long long)row * LD + col] = v.lo;
   Glo[(long long)col * LD + row] = v.lo;
+}
+
+__device__ __forceinline__ void upper_block(int blk, int nb, int& bi, int& bj) {
+  bi = 0;
+  while (blk >= nb - bi) { blk -= nb - bi; ++bi; }
+  bj = bi + blk;
+}
+
+// fixed white noise, one-off (ewh_create / ewh_set_fixed_white): the cached
+// Gram for the double-double timing-model elimination (schur_kernel).  One
+// fp64 MFMA accumulator over 20k TOAs had moved prior-draw lnL by up to 7e-2
+// on C3 through the ill-conditioned elimination (round 2,
+// tests/test_gpu_parity.py::test_c3_bench_workload_prior_draws).  (Chromatic
+// `vary` bases never take this path: their basis is theta-dependent, so white
+// noise is not cached.)
+__global__ __launch_bounds__(256) void gram_dd_kernel(PsrDev P, const double* __restrict__ Xlo,
+                                                      const double* __restrict__ w,
+                                                      const double* __restrict__ beta, double* __restrict__ G,
+                                                      double* __restrict__ Glo) {
+  __shared__ double Ta[32][17], Tb[32][17], Ua[32][17], Ub[32][17], wv[32];
+  int bi, bj;
+  upper_block(blockIdx.x, P.nb, bi, bj);
+  gram_dd_block(P, Xlo, w, beta, bi, bj, G, Glo, Ta, Tb, Ua, Ub, wv);
+}
+
+// Round 6: the same Gram for the varying-white-noise units whose fp64
+// factorisation failed (a pivot <= 0: an -inf term), listed by the failure
+// scan (verify_units_kernel on the unit terms alone).  The exact Sigma of a
+// full-rank basis is positive definite, so such an -inf is a rounding failure
+// of the fp64 Gram or factorisation; the unit is refactored by chol_dd_kernel
+// on this G_hi + G_lo (tests/test_gpu_parity.py::
+// test_c4_bench_inf_sets_at_scale).  Grid (upper blocks, list slots): slot y
+// takes list entries y, y + gridDim.y, ...; unit u -> sample b = u % B, row
+// j = b - b_off of the chunk's per-sample weights / beta and of G (stride
+// ld^2).
+__global__ __launch_bounds__(256) void gram_dd_units_kernel(PsrDev P, const double* __restrict__ Xlo,
+                                                            const double* __restrict__ w,
+                                                            const double* __restrict__ beta,
+                                                            const int* __restrict__ list,
+                                                            const int* __restrict__ count, int B, int b_off,
+                                                            double* __restrict__ G, double* __restrict__ Glo) {
+  __shared__ double Ta[32][17], Tb[32][17], Ua[32][17], Ub[32][17], wv[32];
+  int bi, bj;
+  upper_block(blockIdx.x, P.nb, bi, bj);
+  const int cnt = *count;
+  const long long LD2 = (long long)P.ld * P.ld;
+  for (int y = blockIdx.y; y < cnt; y += gridDim.y) {
+    const int jb = list[y] % B - b_off;
+    gram_dd_block(P, Xlo, w + (long long)jb * P.n_toa, beta + (long long)jb * P.n_epoch, bi, bj, G + jb * LD2,
+                  Glo + jb * LD2, Ta, Tb, Ua, Ub, wv);
+  }
 }
 
 // ----------------------------------------------------------------------------
@@ -235,6 +321,7 @@ __global__ __launch_bounds__(256) void schur_kernel(double* Ghi, double* Glo, in
                                                     const DSpec* __restrict__ spec,
                                                     double Kb, double* S, int fx_ld, int nloc, int gstart,
                                                     int ncommon, double* Kout, int* fail_out, double* Slo) {
+#pragma clang fp contract(off)   // (double-double elimination: ewarp_dev.h)
   __shared__ double rh[256 * 4], rl[256 * 4];
   __shared__ double red[4];
   double lphi = 0.0;
@@ -1442,6 +1529,12 @@ struct PsrHost {
   double* d_S = nullptr;          // fx_ld^2
   double* d_Slo = nullptr;        // fx_ld^2, the low part of S (dd_path pulsars only)
   double* d_Srev = nullptr;       // fx_ld^2, fl(S + 2 S_lo): the reversed verify pass's input (with d_Slo)
+  // the projection residual X_lo of T_aug (round 6; the layout of dev.T,
+  // zero outside the projected columns): dev.T + d_Tlo = T - M C to double-
+  // double, read by the double-double Grams (gram_dd_block).  NULL for
+  // pulsars with a theta-dependent basis (n_bgroup > 0) or the correlated
+  // varying-WN layout
+  double* d_Tlo = nullptr;
   bool has_theta_white = false;
   int n_slot = 0;
   ewh_pref* d_slots = nullptr;    // device copy of the white-noise slot table (PsrDev::slots)
@@ -1486,11 +1579,11 @@ struct DevCtx {
   size_t units2_cap = 0;
   int* d_ddlist = nullptr;       // the verify step's flagged units, [0] = count, list from [1]
   size_t ddlist_cap = 0;
-  // ewh_refine_stats since the last query: device counters [0] units
-  // chol_dd_kernel refactored, [1] units verified (counted by the verify
-  // kernel, so graph replays count too); MODE_DD's units on the host
-  int* d_ddstat = nullptr;
-  long long dd_forced = 0;
+  // ewh_refine_stats since the last query: 64-bit device counters [0] units
+  // chol_dd_kernel refactored, [1] units that took the double-double route --
+  // counted in stream order by the verify kernel (or, kernel mode 29, by
+  // count_units_kernel), so graph replays count and captures do not
+  unsigned long long* d_ddstat = nullptr;
   double* d_Glo = nullptr;       // varying white noise, bases past 16 blocks: the low part of G (contract_wide_kernel)
   int chunk = 0;
   int chunk_cap = 0;          // largest chunk the ~1.5 GB scratch budget allows
@@ -1703,8 +1796,14 @@ constexpr int MODE_WIDE = 27, MODE_DD = 29;
 // 4096 system-model prior draws through at up to 4.4x strict from double-
 // double): near-truth draws stay on fp64 MFMA, the ill-conditioned prior
 // draws get the double-double value)
+// Round 6: MODE_DD also takes the fixed-white-noise pulsars at the register
+// kernels' widths (nb <= 9: the headline C3 model), so the headline batch has a
+// device-side double-double twin (tests/test_gpu_parity.py::
+// test_headline_matches_dd_at_scale); their S_lo is kept from the mode's
+// setting on (ewh_set_kernel_mode re-runs setup_fixed)
 bool dd_path(const DevCtx* h, int nb, bool fixed) {
   if (h->corr || h->osmode || h->kernel_mode == MODE_WIDE || h->kernel_mode == 1) return false;
+  if (h->kernel_mode == MODE_DD && fixed) return true;
   return nb > BIG_NB_MAX || (fixed && nb > MFMA_NB_MAX);
 }
 
@@ -1796,15 +1895,15 @@ int launch_dd_path(DevCtx* h, int nb, const CholJob* jobs, int B, long long u0, 
   const long long cap = ensure_dd_scratch(h, 16 * nb);
   if (cap <= 0) return EWH_E_NOMEM;
   const long long per = dd_scratch_per_wg(16 * nb);
-  if (h->kernel_mode == MODE_DD) {
-    h->dd_forced += n;
-    return launch_chol_dd(jobs, B, u0, n, b_off, theta, ldth, units, h->d_ddscr, per, cap, 16 * nb, st,
-                          h->kernel_mode == MODE_WIDE_R05A);
-  }
   int rc;
   if (!h->d_ddstat) {
     if ((rc = dalloc(h, &h->d_ddstat, 2))) return rc;
-    EWH_HIP(hipMemsetAsync(h->d_ddstat, 0, 2 * sizeof(int), st));
+    EWH_HIP(hipMemsetAsync(h->d_ddstat, 0, 2 * sizeof(unsigned long long), st));
+  }
+  if (h->kernel_mode == MODE_DD) {
+    if ((rc = launch_count_units(h->d_ddstat, n, st))) return rc;
+    return launch_chol_dd(jobs, B, u0, n, b_off, theta, ldth, units, h->d_ddscr, per, cap, 16 * nb, st,
+                          h->kernel_mode == MODE_WIDE_R05A);
   }
   const size_t U = (size_t)(h->P + (h->corr ? 1 : 0)) * B;
   if ((rc = ensure_buf(h, &h->d_units2, &h->units2_cap, U)) || (rc = ensure_buf(h, &h->d_ddlist, &h->ddlist_cap, U + 1)))
@@ -1827,6 +1926,48 @@ int launch_dd_path(DevCtx* h, int nb, const CholJob* jobs, int B, long long u0, 
   if ((rc = launch_verify_units(units, h->d_units2, u0, n, h->d_ddlist + 1, h->d_ddlist, h->d_ddstat, st))) return rc;
   return launch_chol_dd_list(jobs, B, b_off, theta, ldth, units, h->d_ddscr, per, std::min<long long>(cap, n),
                              h->d_ddlist + 1, h->d_ddlist, 16 * nb, st, h->kernel_mode == MODE_WIDE_R05A);
+}
+
+// Round 6: an -inf unit term from an fp64 factorisation is a rounding failure
+// wherever the exact Sigma is positive definite (every full-rank basis: T^T
+// N^-1 T + diag(phi^-1)), so the units [u0, u0 + n) whose term is not finite
+// are listed (verify_units_kernel on the terms alone) and refactored by
+// chol_dd_kernel on a double-double matrix: the cached S_hi + S_lo (fixed
+// white noise), or G_hi + G_lo of those samples from gram_dd_units_kernel
+// (varying white noise: psr != NULL, the chunk's weights in h->d_w / d_beta).
+// The -inf that remains is the double-double factorisation's (or a failed
+// timing-model block, CholJob::fail).  Four launches per run, empty lists exit
+// at once.  Not in the cross-check modes 1 / 27 (fp64 kernels compared as such).
+bool refine_on(const DevCtx* h) {
+  return !h->corr && !h->osmode && h->kernel_mode != 1 && h->kernel_mode != MODE_WIDE;
+}
+
+int refine_failed(DevCtx* h, const CholJob* jobs, int nb, int B, long long u0, long long n, int b_off,
+                  const double* theta, int ldth, double* units, hipStream_t st, const PsrHost* psr) {
+  if (n <= 0) return 0;
+  const long long cap = ensure_dd_scratch(h, 16 * nb);
+  if (cap <= 0) return EWH_E_NOMEM;
+  int rc;
+  if (!h->d_ddstat) {
+    if ((rc = dalloc(h, &h->d_ddstat, 2))) return rc;
+    EWH_HIP(hipMemsetAsync(h->d_ddstat, 0, 2 * sizeof(unsigned long long), st));
+  }
+  const size_t U = (size_t)(h->P + (h->corr ? 1 : 0)) * B;
+  if ((rc = ensure_buf(h, &h->d_ddlist, &h->ddlist_cap, U + 1))) return rc;
+  EWH_HIP(hipMemsetAsync(h->d_ddlist, 0, sizeof(int), st));
+  // (kernel mode 29: every unit listed -- the double-double twin of these routes)
+  if ((rc = launch_verify_units(units, units, u0, n, h->d_ddlist + 1, h->d_ddlist, h->d_ddstat, st,
+                                h->kernel_mode == MODE_DD)))
+    return rc;
+  if (psr) {
+    const int nbk = psr->nb * (psr->nb + 1) / 2;
+    const unsigned slots = (unsigned)std::min<long long>(n, 64);
+    hipLaunchKernelGGL(gram_dd_units_kernel, dim3(nbk, slots), dim3(256), 0, st, psr->dev, psr->d_Tlo, h->d_w, h->d_beta,
+                       h->d_ddlist + 1, h->d_ddlist, B, b_off, h->d_G, h->d_Glo);
+    EWH_HIP(hipGetLastError());
+  }
+  return launch_chol_dd_list(jobs, B, b_off, theta, ldth, units, h->d_ddscr, dd_scratch_per_wg(16 * nb),
+                             std::min<long long>(cap, n), h->d_ddlist + 1, h->d_ddlist, 16 * nb, st, false);
 }
 
 // the partial factorisation (correlated common process) of units [u0, u0 + n)
@@ -1916,8 +2057,10 @@ int ensure_var_scratch(DevCtx* h, int B) {
   // epoch-sum rows per sample: whole CT_ROWS tiles (+1) so the pipelined
   // contraction's last epoch tile reads zero-initialised pad rows
   const size_t sstride = ((maxe + CT_ROWS - 1) / CT_ROWS + 1) * CT_ROWS * maxld;
-  const bool wide = maxld > 16 * BIG_NB_MAX;        // G_lo for the double-double factorisation
-  const size_t per = ((wide ? 2 : 1) * maxld * maxld + sstride + maxn + maxe + maxfac + 1) * sizeof(double);
+  const bool wide = maxld > 16 * BIG_NB_MAX;
+  // G_lo for the double-double factorisation: of every unit past 16 blocks,
+  // and (round 6) of the units whose fp64 factorisation fails (refine_failed)
+  const size_t per = (2 * maxld * maxld + sstride + maxn + maxe + maxfac + 1) * sizeof(double);
   // (bases past 16 blocks: 8 GB of the 288 GB HBM, so a batch of up to 1024
   // samples is one chunk -- one GEMM-form contraction over all of it and one
   // factorisation launch with 4 units per CU instead of 4 launches of 256
@@ -1940,7 +2083,7 @@ int ensure_var_scratch(DevCtx* h, int B) {
   if ((rc = dalloc(h, &h->d_rho, chunk))) return rc;
   if ((rc = dalloc(h, &h->d_fac, chunk * maxfac))) return rc;
   h->d_Glo = nullptr;
-  if (wide && (rc = dalloc(h, &h->d_Glo, chunk * maxld * maxld))) return rc;
+  if ((rc = dalloc(h, &h->d_Glo, chunk * maxld * maxld))) return rc;
   h->chunk = (int)chunk;
   std::vector<CholJob> jobs(h->P);
   for (int p = 0; p < h->P; ++p) {
@@ -1949,7 +2092,7 @@ int ensure_var_scratch(DevCtx* h, int B) {
     // common block is assembled globally)
     const int mreal = h->corr ? ps.gstart_v : ps.m;
     jobs[p] = CholJob{h->d_G, (long long)ps.ld * ps.ld, ps.ld, mreal, ps.d_colptr, ps.d_spec, h->d_Kb, 1, 0};
-    if (ps.nb > BIG_NB_MAX) jobs[p].mats_lo = h->d_Glo;
+    jobs[p].mats_lo = h->d_Glo;
   }
   EWH_HIP(hipMemcpy(h->d_jobs_var, jobs.data(), sizeof(CholJob) * h->P, hipMemcpyHostToDevice));
   return 0;
@@ -2043,8 +2186,10 @@ int setup_fixed(DevCtx* h) {
     if (ps.n_epoch > 0)
       hipLaunchKernelGGL(epoch_sums_kernel, dim3(ps.n_epoch, 1), dim3(256), 0, h->stream, ps.dev, w, nullptr, s);
     if (ps.dev.n_bgroup == 0 && h->kernel_mode != 7) {
-      hipLaunchKernelGGL(gram_dd_kernel, dim3(ps.nb * (ps.nb + 1) / 2), dim3(256), 0, h->stream, ps.dev, w, beta, s, G,
-                         Glo);
+      // (the exactly projected basis: T_aug + its projection residual d_Tlo;
+      // the epoch sums formed inside from both)
+      hipLaunchKernelGGL(gram_dd_kernel, dim3(ps.nb * (ps.nb + 1) / 2), dim3(256), 0, h->stream, ps.dev, ps.d_Tlo, w,
+                         beta, G, Glo);
       EWH_HIP(hipGetLastError());
     } else {
       EWH_HIP(hipMemsetAsync(Glo, 0, sizeof(double) * (size_t)ps.ld * ps.ld, h->stream));
@@ -2054,9 +2199,10 @@ int setup_fixed(DevCtx* h) {
     EWH_HIP(hipMemcpyAsync(&Kb_h, Kb, sizeof(double), hipMemcpyDeviceToHost, h->stream));
     EWH_HIP(hipStreamSynchronize(h->stream));
     if (!ps.d_S && (rc = dalloc(h, &ps.d_S, (size_t)ps.fx_ld * ps.fx_ld))) return rc;
-    // the low part of S for the double-double factorisation (uncorrelated
-    // bases past the register kernels, dd_path)
-    if (!ps.d_Slo && dd_path(h, ps.fx_nb, true) && (rc = dalloc(h, &ps.d_Slo, (size_t)ps.fx_ld * ps.fx_ld))) return rc;
+    // the low part of S for the double-double factorisation: bases past the
+    // register kernels (dd_path), and (round 6) every unit whose fp64
+    // factorisation fails (refine_failed)
+    if (!ps.d_Slo && (rc = dalloc(h, &ps.d_Slo, (size_t)ps.fx_ld * ps.fx_ld))) return rc;
     if (ps.d_Slo && !ps.d_Srev && (rc = dalloc(h, &ps.d_Srev, (size_t)ps.fx_ld * ps.fx_ld))) return rc;
     hipLaunchKernelGGL(schur_kernel, dim3(1), dim3(256), 0, h->stream, G, Glo, ps.ld, ps.m, ps.nlead, ps.d_colptr,
                        ps.d_spec, Kb_h, ps.d_S, ps.fx_ld, ps.nloc, ps.gstart, ps.ncommon, h->d_fxK + p,
@@ -2500,17 +2646,32 @@ ProjCoef projection_coef(const ewh_pulsar_desc& s) {
   return pc;
 }
 
-// X' = X - M C on T_aug (row-major, leading dimension ld, residual at ld-1)
-void apply_projection(const ProjCoef& pc, int n_toa, int ld, std::vector<double>& Ta) {
+// X' = X - M C on T_aug (row-major, leading dimension ld, residual at ld-1),
+// formed in double-double (round 6): TwoProd of each M_ta C_ak (by fma) and
+// TwoSum into (s, e), so s + e = X - M C to ~2^-106; T_aug takes the rounded
+// value fl(s + e) and, when lo is given, lo takes the residual (s + e) -
+// fl(s + e), the part of the exact projection that the fp64 T_aug drops
+// (rounds 2-5: one fma chain, its rounding -- up to eps |M C|, cancellation
+// included -- entered every Gram)
+void apply_projection(const ProjCoef& pc, int n_toa, int ld, std::vector<double>& Ta, std::vector<double>* lo) {
+#pragma clang fp contract(off)
   const int nl = pc.nl, nc = (int)pc.cols.size() + 1;
   if (nl == 0) return;
   for (int t = 0; t < n_toa; ++t) {
     double* row = &Ta[(size_t)t * ld];
     for (int k = 0; k < nc; ++k) {
       const int col = k < nc - 1 ? pc.cols[k] : ld - 1;
-      double v = row[col];
-      for (int a = 0; a < nl; ++a) v = std::fma(-row[a], pc.C[(size_t)a * nc + k], v);
+      double hs = row[col], es = 0.0;
+      for (int a = 0; a < nl; ++a) {
+        const double p = -row[a] * pc.C[(size_t)a * nc + k];
+        const double pe = std::fma(-row[a], pc.C[(size_t)a * nc + k], -p);   // -M C = p + pe exactly
+        const double sum = hs + p, bp = sum - hs;
+        es += ((hs - (sum - bp)) + (p - bp)) + pe;                           // TwoSum error + product error
+        hs = sum;
+      }
+      const double v = hs + es;
       row[col] = v;
+      if (lo) (*lo)[(size_t)t * ld + col] = (hs - v) + es;                   // (hs - v exact: v ~ hs)
     }
   }
 }
@@ -2592,7 +2753,11 @@ int create_ctx(const ewh_pta_desc* d, const std::vector<ProjCoef>& proj, int dev
       Ta[(size_t)t * ps.ld + ps.ld - 1] = s.resid[t];
       sig2[t] = s.toaerr[t] * s.toaerr[t];
     }
-    apply_projection(proj[p], s.n_toa, ps.ld, Ta);
+    // the projection residual for the double-double Grams (PsrHost::d_Tlo)
+    const bool want_lo = !corr_var && s.n_bgroup == 0 && proj[p].nl > 0;
+    std::vector<double> Tlo(want_lo ? Ta.size() : 0, 0.0);
+    apply_projection(proj[p], s.n_toa, ps.ld, Ta, want_lo ? &Tlo : nullptr);
+    if (want_lo && (rc = dupload(h, &ps.d_Tlo, Tlo.data(), Tlo.size()))) return bail(rc);
     if (corr_var) {       // common columns to their block-aligned positions (from the top: pos >= j)
       for (int t = 0; t < s.n_toa; ++t) {
         double* row = &Ta[(size_t)t * ps.ld];
@@ -2746,6 +2911,10 @@ int ctx_units(DevCtx* h, const double* theta_dev, int B, int64_t u_begin, int64_
           (rc = dispatch_chol(h, nb0, maxm, h->d_jobs_fixed, B, u, seg_end - u, 0, theta_dev, ldth, h->d_units, st,
                               true)))
         return rc;
+      if (!dd_path(h, nb0, true) && refine_on(h) &&
+          (rc = refine_failed(h, h->d_jobs_fixed, nb0, B, u, seg_end - u, 0, theta_dev, ldth, h->d_units, st,
+                              nullptr)))
+        return rc;
       u = seg_end;
     }
   } else {
@@ -2760,6 +2929,11 @@ int ctx_units(DevCtx* h, const double* theta_dev, int B, int64_t u_begin, int64_
         if ((rc = ensure_big_scratch(h, h->psr[p].nb)) ||
             (rc = dispatch_chol(h, h->psr[p].nb, h->psr[p].m, h->d_jobs_var, B, (long long)p * B + c0, nb, c0,
                                 theta_dev, ldth, h->d_units, st, false)))
+          return rc;
+        const PsrHost& ps = h->psr[p];
+        if (!dd_path(h, ps.nb, false) && ps.dev.n_bgroup == 0 && refine_on(h) &&
+            (rc = refine_failed(h, h->d_jobs_var, ps.nb, B, (long long)p * B + c0, nb, c0, theta_dev, ldth,
+                                h->d_units, st, &ps)))
           return rc;
       }
       u = pend;
@@ -3237,15 +3411,22 @@ int lnl_batch_single(ewh_handle* H, DevCtx* h, int B, double* out_host) {
                                         " ran out (LAT_SPIN_MAX); no lnL was produced");
         }
       // lnL_b = sum over pulsars in pulsar order (reduce_units_kernel's fold)
+      bool failed = false;
       for (int b = 0; b < B; ++b) {
         double s = 0.0;
         for (int p = 0; p < h->P; ++p) s += H->h_out[(size_t)p * B + b];
         out_host[b] = s;
+        failed = failed || !std::isfinite(s);
       }
-      H->last_split.assign(1, {0, (long long)H->P * B});
-      H->last_B = B;
-      h->last_B = B;
-      return 0;
+      // an fp64 pivot failure (-inf term) is refactored in double-double by
+      // the batched path (refine_failed): take it for this call instead
+      if (!failed) {
+        H->last_split.assign(1, {0, (long long)H->P * B});
+        H->last_B = B;
+        h->last_B = B;
+        return 0;
+      }
+      EWH_HIP(hipStreamSynchronize(h->stream));
     }
   }
   if ((rc = ensure_io(h, B))) return rc;
@@ -3381,15 +3562,16 @@ int ewh_refine_stats(ewh_handle* H, int64_t* checked, int64_t* refined) {
   long long c = 0, r = 0;
   for (DevCtx* h : H->ctx) {
     EWH_HIP(hipSetDevice(h->device));
-    EWH_HIP(hipStreamSynchronize(h->stream));
-    int v[2] = {0, 0};
+    // (the whole device: ewh_lnl_units_device runs the route on the caller's
+    // stream, whose work must be counted before the reset)
+    EWH_HIP(hipDeviceSynchronize());
+    unsigned long long v[2] = {0, 0};
     if (h->d_ddstat) {
-      EWH_HIP(hipMemcpy(v, h->d_ddstat, 2 * sizeof(int), hipMemcpyDeviceToHost));
-      EWH_HIP(hipMemset(h->d_ddstat, 0, 2 * sizeof(int)));
+      EWH_HIP(hipMemcpy(v, h->d_ddstat, sizeof v, hipMemcpyDeviceToHost));
+      EWH_HIP(hipMemset(h->d_ddstat, 0, sizeof v));
     }
-    c += h->dd_forced + v[1];
-    r += h->dd_forced + v[0];
-    h->dd_forced = 0;
+    c += (long long)v[1];
+    r += (long long)v[0];
   }
   if (checked) *checked = c;
   if (refined) *refined = r;
@@ -3437,7 +3619,11 @@ int ewh_set_kernel_mode(ewh_handle* H, int32_t mode) {
     (void)hipSetDevice(h->device);
     drop_graphs(h);
     const bool stage = mode != 19;   // dev mode 19: the register kernels' CSR spectrum prologue
-    if (stage != h->stage_spectra) {
+    // MODE_DD on a pulsar whose S_lo was not kept (register widths): set up again
+    bool need_lo = false;
+    if (h->white_fixed)
+      for (const auto& ps : h->psr) need_lo = need_lo || (!ps.d_Slo && dd_path(h, ps.fx_nb, true));
+    if (stage != h->stage_spectra || need_lo) {
       h->stage_spectra = stage;
       if (h->white_fixed) {
         const int rc = setup_fixed(h);
@@ -3694,6 +3880,34 @@ int ewh_dev_gram(ewh_handle* H, int32_t p, const double* theta_host, int32_t B, 
   EWH_HIP(hipStreamSynchronize(h->stream));
   const int ld = h->psr[p].ld;
   EWH_HIP(hipMemcpy(G_out, h->d_G, sizeof(double) * (size_t)B * ld * ld, hipMemcpyDeviceToHost));
+  return ld;
+}
+
+// the double-double G_hi / G_lo of gram_dd_units_kernel (the fp64-failure
+// refinement, varying white noise) of pulsar p for samples [0, B); returns ld
+int ewh_dev_gram_dd(ewh_handle* H, int32_t p, const double* theta_host, int32_t B, double* G_out, double* Glo_out) {
+  DevCtx* h = H->ctx[0];
+  if (p < 0 || p >= h->P || B <= 0 || h->white_fixed) return set_err(EWH_E_INVALID, "bad arguments");
+  int rc;
+  EWH_HIP(hipSetDevice(h->device));
+  if ((rc = ensure_var_scratch(h, B))) return rc;
+  if (B > h->chunk) return set_err(EWH_E_INVALID, "B exceeds the varying-WN chunk");
+  if ((rc = ensure_io(h, B)) || (rc = ensure_units(h, B))) return rc;
+  EWH_HIP(hipMemcpy(h->d_theta, theta_host, sizeof(double) * (size_t)B * h->n_param, hipMemcpyHostToDevice));
+  if ((rc = run_white(h, p, h->d_theta, h->n_param, 0, B))) return rc;
+  std::vector<int> lst(B + 1);
+  lst[0] = B;
+  for (int b = 0; b < B; ++b) lst[b + 1] = p * B + b;
+  const size_t U = (size_t)(h->P + 1) * B;
+  if ((rc = ensure_buf(h, &h->d_ddlist, &h->ddlist_cap, U + 1))) return rc;
+  EWH_HIP(hipMemcpy(h->d_ddlist, lst.data(), sizeof(int) * (B + 1), hipMemcpyHostToDevice));
+  const PsrHost& ps = h->psr[p];
+  hipLaunchKernelGGL(gram_dd_units_kernel, dim3(ps.nb * (ps.nb + 1) / 2, std::min(B, 64)), dim3(256), 0, h->stream,
+                     ps.dev, ps.d_Tlo, h->d_w, h->d_beta, h->d_ddlist + 1, h->d_ddlist, B, 0, h->d_G, h->d_Glo);
+  EWH_HIP(hipStreamSynchronize(h->stream));
+  const int ld = ps.ld;
+  EWH_HIP(hipMemcpy(G_out, h->d_G, sizeof(double) * (size_t)B * ld * ld, hipMemcpyDeviceToHost));
+  EWH_HIP(hipMemcpy(Glo_out, h->d_Glo, sizeof(double) * (size_t)B * ld * ld, hipMemcpyDeviceToHost));
   return ld;
 }
 

@@ -54,7 +54,7 @@
 extern "C" {
 #endif
 
-#define EWH_ABI_VERSION 6
+#define EWH_ABI_VERSION 7
 
 enum ewh_status {
   EWH_OK = 0,
@@ -264,13 +264,17 @@ double ewh_unit_cost(const ewh_handle* h, int32_t pulsar);
 int ewh_transfer_stats(const ewh_handle* h, int64_t* h2d_bytes, int64_t* peer);
 
 /* The double-double route since the last query (bases past the register
- * kernels: fixed white noise past 9 blocks, any basis past 16):
- * *checked = units that took it, *refined = units chol_dd_kernel refactored
- * (the verify step flagged them -- the forward and reversed fp64
- * factorisations disagree by more than a quarter of strict -- or kernel mode
- * 29 sent every unit; those are counted at launch, so not in replays of a
- * captured ewh_lnl_batch graph).  Synchronises the handle's streams and
- * resets both counts.  Either pointer may be NULL.  (Host twin: always 0.) */
+ * kernels: fixed white noise past 9 blocks, any basis past 16; under kernel
+ * mode 29 every fixed-white-noise unit): *checked = units that took it,
+ * *refined = units chol_dd_kernel refactored (the verify step flagged them --
+ * the forward and reversed fp64 factorisations disagree by more than
+ * VERIFY_FRAC = 1/16 of strict, csrc/chol_dd.hip -- or kernel mode 29 sent
+ * every unit).  Both are 64-bit counters kept on the device in stream order:
+ * replays of a captured ewh_lnl_batch graph count, the capture itself does
+ * not.  Synchronises every device of the handle (all streams, so work the
+ * caller enqueued with ewh_lnl_units_device on its own stream is counted)
+ * and resets both counts.  Either pointer may be NULL.  (Host twin: always
+ * 0.)  ABI 7. */
 int ewh_refine_stats(ewh_handle* h, int64_t* checked, int64_t* refined);
 
 /* Kernel selection: 0 = auto (register-blocked MFMA factorisation with the
@@ -288,7 +292,9 @@ int ewh_refine_stats(ewh_handle* h, int64_t* checked, int64_t* refined);
  * any-width chol_wide_kernel (cross-check of the register, big and
  * double-double kernels), 29 = the double-double factorisation for every unit
  * of a basis past the register kernels (default: only where the forward and
- * reversed fp64 factorisations disagree), 7 = default factorisation with the
+ * reversed fp64 factorisations disagree) and, with fixed white noise, for
+ * every unit at the register kernels' widths too (the device-side
+ * double-double twin of the headline batch; ABI 7), 7 = default factorisation with the
  * round-1 kernels
  * elsewhere: the contraction (varying white noise: separate epoch-sum
  * kernel, unpipelined tiles) instead of the pipelined one and, for a

@@ -84,14 +84,27 @@ def dd_of(a):
 
 
 # ---- model pieces -----------------------------------------------------------
-def dd_gram(X, w):
+# 18-bit slices per operand column (device_order_ref._slices): k slices hold
+# 18 k bits below the column's largest entry, the rest is dropped.  Round 6:
+# k = 6 (108 bits: every fp64 entry within 2^-55 of its column maximum is
+# represented exactly, and the dropped remainder is below 2^-108 of the
+# column maximum -- double-double level).  Rounds 4-5 used k = 4 (72 bits): a
+# truncation of ~2^-72 relative to the column maximum, which on the most
+# ill-conditioned prior draws moved lnl_exact by up to ~0.7 % of strict
+# (scripts/ddref_yardstick.py).
+DD_SLICES = 6
+
+
+def dd_gram(X, w, k=None):
     """G = X^T diag(w) X with w a double-double vector: X w_hi = A_hi + A_lo
-    exactly (TwoProduct), A_hi^T X error free (18-bit slices: exact fp64
-    products and sums, combined in double-double), the remainder
-    (A_lo + X w_lo)^T X by one fp64 product (a 2^-106-relative term)."""
+    exactly (TwoProduct), A_hi^T X error free to 2^-18k of the column maxima
+    (18-bit slices: exact fp64 products and sums, combined in double-double),
+    the remainder (A_lo + X w_lo)^T X by one fp64 product (a 2^-106-relative
+    term)."""
+    k = DD_SLICES if k is None else k
     A_hi, A_lo = two_prod(X, w[0][:, None])
     A_lo = A_lo + X * w[1][:, None]
-    SA, SB = _slices(A_hi), _slices(X)
+    SA, SB = _slices(A_hi, k), _slices(X, k)
     k = len(SA)
     acc = (np.zeros((X.shape[1], X.shape[1])), np.zeros((X.shape[1], X.shape[1])))
     for s in range(k):
@@ -100,11 +113,12 @@ def dd_gram(X, w):
     return dd_add(acc, dd_of(A_lo.T @ X))
 
 
-def dd_matmul_tn(A, B):
+def dd_matmul_tn(A, B, k=None):
     """A^T B for double-double matrices (hi, lo): A_hi^T B_hi error free
     (18-bit slices, as dd_gram), A_hi^T B_lo + A_lo^T B_hi by fp64 products
     (2^-53-relative terms of a 2^-53-relative correction)."""
-    SA, SB = _slices(A[0]), _slices(B[0])
+    k = DD_SLICES if k is None else k
+    SA, SB = _slices(A[0], k), _slices(B[0], k)
     k = len(SA)
     acc = (np.zeros((A[0].shape[1], B[0].shape[1])), np.zeros((A[0].shape[1], B[0].shape[1])))
     for s in range(k):

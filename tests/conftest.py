@@ -28,12 +28,14 @@ def pytest_configure(config):
     config.addinivalue_line("markers", "gpu: needs an MI355X (HIP device) and libewarp_hip.so")
     config.addinivalue_line("markers", "gpu_ab: kernel A/B variants (dev library libewarp_hip_dev.so, "
                                        "`make -C enterprise_warp_amd/csrc dev`); not part of the driver's -m gpu suite")
+    config.addinivalue_line("markers", "gpu_debug: the device-side debug build (build/libewarp_hip_debug.so, "
+                                       "`make -C enterprise_warp_amd/csrc debug`); not part of the driver's -m gpu suite")
 
 
 def pytest_collection_modifyitems(config, items):
     skip = pytest.mark.skip(reason="A/B variant tests need a GPU and the dev library (make dev)")
     for it in items:
-        if "gpu_ab" in it.keywords and not gpu_available():
+        if ("gpu_ab" in it.keywords or "gpu_debug" in it.keywords) and not gpu_available():
             it.add_marker(skip)
 
 

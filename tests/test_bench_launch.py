@@ -91,3 +91,34 @@ def test_bench_refuses_world_mismatch():
                        capture_output=True, text=True, timeout=120)
     assert r.returncode != 0
     assert "WORLD_SIZE=2" in r.stderr
+
+
+def test_verify_on_by_default_with_ranks():
+    """a plain multi-rank `bench.py --gpus N` verifies by
+    default (the driver passes no flag); --no-verify / --verify override."""
+    assert bench.verify_default(None, 1) is False
+    assert bench.verify_default(None, 2) is True and bench.verify_default(None, 8) is True
+    assert bench.verify_default(False, 8) is False and bench.verify_default(True, 1) is True
+
+
+def test_run_problems():
+    """Rank 0 exits non-zero when two ranks sit on one device without
+    --same-device, or the verify block is missing / failed."""
+    a = {"index": 0, "pci_bus_id": "0000:05:00.0", "uuid": "u0"}
+    b = {"index": 1, "pci_bus_id": "0000:15:00.0", "uuid": "u1"}
+    ok = {"samples": 256, "max_err_over_strict": 1e-4, "inf_pattern_equal": True}
+    assert bench.run_problems([a, b], False, ok, True) == []
+    assert bench.run_problems([a, dict(a, index=1)], False, ok, True)            # one device twice
+    assert bench.run_problems([a, dict(a, index=1)], True, ok, True) == []       # the rehearsal
+    assert bench.run_problems([a, b], False, None, True)                         # verify missing
+    assert bench.run_problems([a, b], False, dict(ok, max_err_over_strict=2.0), True)
+    assert bench.run_problems([a, b], False, dict(ok, inf_pattern_equal=False), True)
+    assert bench.run_problems([a], False, None, False) == []
+
+
+def test_bench_parser_verify_flags(monkeypatch):
+    """The CLI carries both flags; a rank of a plain `--gpus 2` run gets
+    args.verify True (main() resolves it before anything touches a GPU)."""
+    src = open(os.path.join(ROOT, "bench.py")).read()
+    assert '"--no-verify"' in src and "args.verify = verify_default(args.verify, world)" in src
+    assert 'rec["verify"] = verify' in src and "sys.exit(3)" in src
