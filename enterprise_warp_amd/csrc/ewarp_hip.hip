@@ -1955,9 +1955,11 @@ int refine_failed(DevCtx* h, const CholJob* jobs, int nb, int B, long long u0, l
   const size_t U = (size_t)(h->P + (h->corr ? 1 : 0)) * B;
   if ((rc = ensure_buf(h, &h->d_ddlist, &h->ddlist_cap, U + 1))) return rc;
   EWH_HIP(hipMemsetAsync(h->d_ddlist, 0, sizeof(int), st));
-  // (kernel mode 29: every unit listed -- the double-double twin of these routes)
-  if ((rc = launch_verify_units(units, units, u0, n, h->d_ddlist + 1, h->d_ddlist, h->d_ddstat, st,
-                                h->kernel_mode == MODE_DD)))
+  // (kernel mode 29: every unit listed -- the double-double twin of the fp64
+  // routes; a basis on the double-double path was factored so already, and
+  // only its -inf units are refined here)
+  const bool all = h->kernel_mode == MODE_DD && !dd_path(h, nb, psr == nullptr);
+  if ((rc = launch_verify_units(units, units, u0, n, h->d_ddlist + 1, h->d_ddlist, h->d_ddstat, st, all)))
     return rc;
   if (psr) {
     const int nbk = psr->nb * (psr->nb + 1) / 2;
@@ -2930,8 +2932,12 @@ int ctx_units(DevCtx* h, const double* theta_dev, int B, int64_t u_begin, int64_
             (rc = dispatch_chol(h, h->psr[p].nb, h->psr[p].m, h->d_jobs_var, B, (long long)p * B + c0, nb, c0,
                                 theta_dev, ldth, h->d_units, st, false)))
           return rc;
+        // (past 16 blocks too: the verify route's double-double factorisation
+        // reads the compensated -- not error-free -- G_hi + G_lo of the wide
+        // contraction, so a unit it still leaves at -inf gets the error-free
+        // Gram here)
         const PsrHost& ps = h->psr[p];
-        if (!dd_path(h, ps.nb, false) && ps.dev.n_bgroup == 0 && refine_on(h) &&
+        if (ps.dev.n_bgroup == 0 && refine_on(h) &&
             (rc = refine_failed(h, h->d_jobs_var, ps.nb, B, (long long)p * B + c0, nb, c0, theta_dev, ldth,
                                 h->d_units, st, &ps)))
           return rc;

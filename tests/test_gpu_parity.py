@@ -476,11 +476,12 @@ def test_verify_route_matches_dd_at_scale(require_gpu, case, seed_offset):
     372-column pulsar with white noise fixed and sampled.  Two fp64 orders
     that agree while both are wrong show here: every sample within strict of
     double-double, or else -- against the CPU double-double reference
-    (oracle/ddref.py) -- no further off than both enterprise's own fp64 order
-    and the all-double-double value (the call matched: pta.get_lnlikelihood,
-    bilby_warp.py:35).  Measured at the strict/16 verify threshold
-    (DESIGN.md §10 r05j): 0 / 1 of the two system batches past strict of
-    double-double (2.1x strict from the exact value, enterprise's order 95x)."""
+    (oracle/ddref.py), which the all-double-double twin must meet at strict --
+    no further off than enterprise's own fp64 order (the call matched:
+    pta.get_lnlikelihood, bilby_warp.py:35).  Measured at the strict/16
+    verify threshold with the error-free twin: 4 / 1 / 3 /
+    1 of four 4096-draw system batches past strict, at most 65x strict where
+    enterprise's order is 1118x."""
     import os
     from conftest import ROOT, reference_lnl, strict_tolerance
     if case == "system":
@@ -502,15 +503,21 @@ def test_verify_route_matches_dd_at_scale(require_gpu, case, seed_offset):
     assert np.array_equal(np.isfinite(got), np.isfinite(dd)), "route and double-double differ in finiteness"
     fin = np.isfinite(dd)
     off = np.flatnonzero(fin & (np.abs(got - dd) > strict_tolerance(dd)))
-    assert len(off) <= max(2, len(X) // 1000), f"{case}: {len(off)} of {len(X)} samples past strict of double-double"
+    print(f"{case}, seed offset {seed_offset}: {len(off)} of {len(X)} samples past strict of double-double "
+          f"(refined {r} of {c} units)")
     if len(off):
+        # the all-double-double twin confirmed against the CPU double-double
+        # reference on those samples (round 6: exact to ~1e-3 strict), and the
+        # route no less accurate there than enterprise's own fp64 order
         ent, ext = reference_lnl(pta, X[off], exact="dd")
         s = strict_tolerance(ext)
         e_route, e_ent, e_dd = np.abs(got[off] - ext), np.abs(ent - ext), np.abs(dd[off] - ext)
-        worse = e_route > np.maximum(np.maximum(e_ent, e_dd), s)
+        print(f"  route {np.round(e_route / s, 3)}, all-dd {np.round(e_dd / s, 4)}, enterprise {np.round(e_ent / s, 1)}"
+              f" (x strict from the CPU double-double value)")
+        assert np.all(e_dd <= s), f"{case}: the double-double twin itself is off: {e_dd / s}"
+        worse = e_route > np.maximum(e_ent, s)
         assert not worse.any(), (f"{case}: samples {off[worse]}: route {e_route[worse] / s[worse]} x strict from the "
-                                 f"exact value, enterprise's order {e_ent[worse] / s[worse]}, "
-                                 f"double-double {e_dd[worse] / s[worse]}")
+                                 f"exact value, enterprise's order {e_ent[worse] / s[worse]}")
 
 
 def test_headline_matches_dd_at_scale(require_gpu):
