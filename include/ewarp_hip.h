@@ -292,9 +292,12 @@ int ewh_refine_stats(ewh_handle* h, int64_t* checked, int64_t* refined);
  * any-width chol_wide_kernel (cross-check of the register, big and
  * double-double kernels), 29 = the double-double factorisation for every unit
  * of a basis past the register kernels (default: only where the forward and
- * reversed fp64 factorisations disagree) and, with fixed white noise, for
- * every unit at the register kernels' widths too (the device-side
- * double-double twin of the headline batch; ABI 7), 7 = default factorisation with the
+ * reversed fp64 factorisations disagree) and every other uncorrelated unit
+ * too -- fixed white noise on the double-double S, varying white noise on an
+ * error-free double-double Gram -- the device-side double-double twin of the
+ * batch (ABI 7).  In every mode but 1 / 27 an uncorrelated unit whose fp64
+ * factorisation returns -inf is refactored in double-double (a -inf result
+ * means the double-double factorisation failed too), 7 = default factorisation with the
  * round-1 kernels
  * elsewhere: the contraction (varying white noise: separate epoch-sum
  * kernel, unpipelined tiles) instead of the pipelined one and, for a
