@@ -42,7 +42,7 @@ constexpr size_t contract2_lds(int nb) { return (size_t)(2 * CT_ROWS * 16 * nb +
 
 // waves per sample: 4, or 8 where measured faster (fewer accumulators per
 // wave: more waves per SIMD to hide the k-steps' LDS latency)
-constexpr int contract2_default_waves(int nb) { return nb >= 9 ? 8 : 4; }
+constexpr int contract2_default_waves(int nb) { return nb >= 9 || contract2_comp(nb) == CT_TWOSUM ? 8 : 4; }
 // the run remainder on the last waves (ct_run_start) where the accumulator is
 // single (NB <= 9: C2's ECORR model); the blocked NB >= 10 kernel keeps the
 // round-4 order -- with the remainder moved its spill grew 12 -> 28 B/lane

@@ -487,7 +487,7 @@ constexpr CtOrd ct_order(int nb, int th, int tw) {
 // weight staging, so they take the shorter runs (round 4: the first waves
 // took the extra blocks -- C2's 45 blocks put 6 MFMA blocks AND the epoch
 // sums on waves 0-2; dev mode 35 keeps that order for the A/B).  Used where
-// the accumulator is single (contract2_late: NB <= 9)
+// the accumulator is TwoSum-compensated, round 6; single until then (contract2_late: NB <= 9)
 constexpr int ct_run_start(int nblk, int ws, int v, bool late = true) {
   const int b = nblk / ws, x = nblk % ws;
   return late ? v * b + (v > ws - x ? v - (ws - x) : 0) : v * b + (v < x ? v : x);
@@ -599,11 +599,17 @@ __device__ __forceinline__ void contract2_body(const PsrDev& P, const double* __
   }
   // RSEP: d of column dc (the d waves), blocked like the Gram
   const int dc = DWAVE ? min(tid - 64 * (W - DW), 16 * NG - 1) : 0;
-  double dacc = 0.0, dhi = 0.0;
+  double dacc = 0.0, dhi = 0.0, dlo = 0.0;
   auto flush = [&]() {
     if constexpr (COMP == CT_SINGLE) return;
     if constexpr (DWAVE) {
-      dhi += dacc;
+      if constexpr (COMP == CT_TWOSUM) {        // (d compensated like the Gram)
+        const double sum = dhi + dacc, bp = sum - dhi;
+        dlo += (dhi - (sum - bp)) + (dacc - bp);
+        dhi = sum;
+      } else {
+        dhi += dacc;
+      }
       dacc = 0.0;
     }
     static_for<0, SLOTS>([&](auto SL) {
@@ -717,7 +723,7 @@ __device__ __forceinline__ void contract2_body(const PsrDev& P, const double* __
         int nf = 0;
         // (4 rows per trip beside the blocked accumulator's second register
         // set, which leaves no room for 8)
-        constexpr int ER = COMP == CT_BLOCKED ? 4 : 8;
+        constexpr int ER = COMP != CT_SINGLE ? 4 : 8;
 #pragma unroll
         for (int r0 = 0; r0 < CT_ROWS; r0 += ER) {
           double tc[ER], wc[ER];
@@ -740,7 +746,7 @@ __device__ __forceinline__ void contract2_body(const PsrDev& P, const double* __
       }
       if constexpr (DWAVE) {                         // d of column dc: this tile's rows
         const double* ewr = ewbase + cur * CT_ROWS;
-        constexpr int DR = COMP == CT_BLOCKED ? 4 : 8;     // rows per LDS trip (registers, as the epoch sums)
+        constexpr int DR = COMP != CT_SINGLE ? 4 : 8;     // rows per LDS trip (registers, as the epoch sums)
 #pragma unroll
         for (int r0 = 0; r0 < CT_ROWS; r0 += DR) {
           double tc[DR], wc[DR];
@@ -775,7 +781,7 @@ __device__ __forceinline__ void contract2_body(const PsrDev& P, const double* __
     // the last diagonal block: unit diagonal on the pads, rho at the corner
     const int a = tid - 64 * (W - DW);
     if (a < 16 * NG) {
-      const double d = COMP == CT_SINGLE ? dacc : dhi;
+      const double d = COMP == CT_SINGLE ? dacc : COMP == CT_TWOSUM ? dhi + dlo : dhi;
       Gout[(long long)a * LD + LD - 1] = d;
       Gout[(long long)(LD - 1) * LD + a] = d;
 #pragma unroll
@@ -833,7 +839,14 @@ __global__ __launch_bounds__(64 * W) void contract2_kernel(PsrDev P, const doubl
 // accumulator sets, so 11+ blocks had to split a sample over two workgroups;
 // C4 5.44 k evals/s, vs 6.51 k with one accumulator.)  Dev kernel mode 30:
 // TwoSum at every width up to 10 blocks (A/B).
-constexpr int contract2_comp(int nb) { return nb >= 10 ? CT_BLOCKED : CT_SINGLE; }
+// Round 6: TwoSum groups up to 10 blocks (C2's 9), blocked from 11 on.  The
+// single accumulator C2 had kept since round 4 left 36 of its 4096 bench prior
+// draws less accurate than enterprise's own fp64 order (at most 15x) against
+// the double-double twin; TwoSum: none (worst 0.59), for 17.6 -> 20.8 ms per
+// batch (scripts/c2_accum_ab.py, profiles/r06i).  Past 10 blocks the third
+// accumulator set does not fit one workgroup per sample (round 4: C4 split
+// over two workgroups, -16 %)
+constexpr int contract2_comp(int nb) { return nb >= 11 ? CT_BLOCKED : CT_TWOSUM; }
 
 // ----------------------------------------------------------------------------
 // batched factorisation, MFMA register-blocked: one wave (64 lanes) per unit.
