@@ -246,8 +246,9 @@ def _c4_prior_accuracy(got, ent, ext, label):
     here: the Gram's rounding dominates the error on these draws,
     scripts/diag_varying_error.py) with errors of the same size, so per draw
     either may be the closer one; the exceptions are printed (measured on the
-    whole batches: C2 36 of 4095 at most 15x, C4 26 of 850 at most 29x;
-    DESIGN.md §2).  Where enterprise's order is -inf, the GPU is finite and
+    whole batches: C4 26 of 850 at most 29x; C2, since its contraction takes
+    TwoSum groups, none -- 36 of 4095 at most 15x with the single
+    accumulator).  Where enterprise's order is -inf, the GPU is finite and
     no further from ext than enterprise's worst error over this batch's
     finite draws."""
     from conftest import strict_tolerance
