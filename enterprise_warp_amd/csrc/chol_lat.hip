@@ -30,6 +30,15 @@
 // last workgroup cost ~4k cycles of agent-scope fences and atomics).
 #include "ewarp_dev.h"
 
+// the diagonal chains' row replication (diag_factor_2l REPL): 2 = by the
+// lane swaps of bcast_rows4 (round 6, bit-identical; three interleaved
+// rounds, scripts/lat_lib_ab.sh, profiles/r06l/latency_ab.log: B = 1 / 8 /
+// 24 30.85 / 37.32 / 79.96 -> 30.35 / 36.89 / 78.40 us per call), 1 = by
+// ds_bpermute (until round 5)
+#ifndef EWH_LAT_REPL
+#define EWH_LAT_REPL 2
+#endif
+
 namespace ewh_dev {
 namespace {
 
@@ -180,7 +189,7 @@ __device__ __forceinline__ void lat_flow(LatLds<NB>& S, v4d (&C)[NB][NB], v4d& E
   int* const stall = &S.stall;
   auto factor = [&](auto BBc) {
     constexpr int bb = decltype(BBc)::value;
-    diag_factor_2l<NB, bb, true, true>(C[bb][bb], E, rsr, q, c, ldet, ok, klast);
+    diag_factor_2l<NB, bb, true, EWH_LAT_REPL>(C[bb][bb], E, rsr, q, c, ldet, ok, klast);
     if constexpr (bb < NB - 1) {
       if constexpr (bb >= LAT_NBUF) lat_wait<VAR == LAT_VAR_STALL>(&S.done[bb - LAT_NBUF], 4, stall);
       lds_put(S.Ef[bb % LAT_NBUF], E, lane);
@@ -401,7 +410,7 @@ __device__ __forceinline__ void lat_wave(LatLds<NB>& S, const CholJob& J, const 
   // factor diagonal block BB (owner only); publish E and the scales, or q
   auto factor = [&](auto BBc) {
     constexpr int bb = decltype(BBc)::value;
-    diag_factor_2l<NB, bb, true, true>(C[bb][bb], E, rsr, q, c, ldet, ok, klast);
+    diag_factor_2l<NB, bb, true, EWH_LAT_REPL>(C[bb][bb], E, rsr, q, c, ldet, ok, klast);
     if constexpr (bb < NB - 1) {
       lds_put(S.Ef[0], E, lane);
       static_for<0, 4>([&](auto R) { S.Rf[0][decltype(R)::value][lane] = rsr[decltype(R)::value]; });

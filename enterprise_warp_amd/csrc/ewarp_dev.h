@@ -1022,7 +1022,32 @@ __device__ __forceinline__ double shfl_row_fresh(double x, int c) {
   return __hiloint2double(hi, lo);
 }
 
-template <int NB, int BB, bool RL, bool REPL = false>
+// The four rows of a sub-panel register x (row j = lanes 16 j .. 16 j + 15)
+// broadcast to every 16-lane row by gfx950's lane-swap instructions:
+// v_permlane32_swap of x with a copy gives rows (0, 1, 0, 1) and (2, 3, 2, 3),
+// v_permlane16_swap of each with a copy the four broadcasts -- 6 swaps on the
+// VALU instead of 8 ds_bpermute round trips through the LDS crossbar.  Same
+// values bit for bit.  (In the batched kernel, issue-bound, the extra copies
+// and replica updates cost more than the crossbar: 3.65 -> 3.76 ms, DESIGN.md
+// §4a; the latency kernel waits on the round trip instead.)
+__device__ __forceinline__ void bcast_rows4(double x, double (&R)[4]) {
+  const int lo = __double2loint(x), hi = __double2hiint(x);
+  const auto l32 = __builtin_amdgcn_permlane32_swap(lo, lo, false, false);
+  const auto h32 = __builtin_amdgcn_permlane32_swap(hi, hi, false, false);
+  const auto l01 = __builtin_amdgcn_permlane16_swap(l32[0], l32[0], false, false);
+  const auto h01 = __builtin_amdgcn_permlane16_swap(h32[0], h32[0], false, false);
+  const auto l23 = __builtin_amdgcn_permlane16_swap(l32[1], l32[1], false, false);
+  const auto h23 = __builtin_amdgcn_permlane16_swap(h32[1], h32[1], false, false);
+  R[0] = __hiloint2double(h01[0], l01[0]);
+  R[1] = __hiloint2double(h01[1], l01[1]);
+  R[2] = __hiloint2double(h23[0], l23[0]);
+  R[3] = __hiloint2double(h23[1], l23[1]);
+}
+
+// REPL: 0 = each pivot row broadcast by ds_bpermute when it is needed (the
+// batched kernels); 1 = the sub-panel's four rows replicated up front by
+// ds_bpermute; 2 = replicated by the lane swaps of bcast_rows4
+template <int NB, int BB, bool RL, int REPL = 0>
 __device__ __forceinline__ void diag_factor_2l(v4d& D, v4d& E, double (&rsr)[4], int q, int c, LogAcc& ldet,
                                                bool& ok, int klim) {
   constexpr bool LASTR = RL && BB == NB - 1;          // block row holding the residual
@@ -1039,8 +1064,10 @@ __device__ __forceinline__ void diag_factor_2l(v4d& D, v4d& E, double (&rsr)[4],
     constexpr int kr = decltype(KR)::value;
     constexpr int nk = (LASTR && kr == 3) ? 3 : 4;   // the r column is not pivoted
     double Rr[4];
-    if constexpr (REPL) {
+    if constexpr (REPL == 1) {
       static_for<0, 4>([&](auto J) { Rr[decltype(J)::value] = __shfl(D[kr], 16 * decltype(J)::value + c); });
+    } else if constexpr (REPL == 2) {
+      bcast_rows4(D[kr], Rr);
     }
     static_for<0, nk>([&](auto KQc) {
       constexpr int kq = decltype(KQc)::value;
