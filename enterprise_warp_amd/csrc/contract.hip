@@ -60,6 +60,15 @@ int launch_contract2(int waves, const PsrDev& P, const double* w, const double* 
                          contract2_lds(NB), st, P, w, beta, s, s_stride, G, nullptr);
       return 0;
     }
+    if (waves == 38 || waves == 39) {   // (dev A/B: blocked accumulation, 4 / 8 waves)
+      if (waves == 39)
+        hipLaunchKernelGGL(HIP_KERNEL_NAME(contract2_kernel<NB, 8, CT_BLOCKED, contract2_late(NB)>), dim3(nb_samples),
+                           dim3(512), contract2_lds(NB), st, P, w, beta, s, s_stride, G, nullptr);
+      else
+        hipLaunchKernelGGL(HIP_KERNEL_NAME(contract2_kernel<NB, 4, CT_BLOCKED, contract2_late(NB)>), dim3(nb_samples),
+                           dim3(256), contract2_lds(NB), st, P, w, beta, s, s_stride, G, nullptr);
+      return 0;
+    }
   }
   if (waves == 35) {     // (dev A/B: the extra blocks on the first waves, round 4-5a)
     if (contract2_default_waves(NB) == 8)
@@ -119,9 +128,14 @@ int set_attr2() {
                                 hipFuncAttributeMaxDynamicSharedMemorySize, (int)contract2_lds(NB)));
   }
 #ifdef EWH_DEV
-  if constexpr (NB <= 10)
+  if constexpr (NB <= 10) {
     EWH_HIP(hipFuncSetAttribute((const void*)contract2_kernel<NB, 8, CT_TWOSUM>,
                                 hipFuncAttributeMaxDynamicSharedMemorySize, (int)contract2_lds(NB)));
+    EWH_HIP(hipFuncSetAttribute((const void*)contract2_kernel<NB, 4, CT_BLOCKED, contract2_late(NB)>,
+                                hipFuncAttributeMaxDynamicSharedMemorySize, (int)contract2_lds(NB)));
+    EWH_HIP(hipFuncSetAttribute((const void*)contract2_kernel<NB, 8, CT_BLOCKED, contract2_late(NB)>,
+                                hipFuncAttributeMaxDynamicSharedMemorySize, (int)contract2_lds(NB)));
+  }
   EWH_HIP(hipFuncSetAttribute((const void*)contract2_kernel<NB, 4, CP, false>,
                               hipFuncAttributeMaxDynamicSharedMemorySize, (int)contract2_lds(NB)));
   EWH_HIP(hipFuncSetAttribute((const void*)contract2_kernel<NB, 8, CP, false>,

@@ -2110,15 +2110,17 @@ int run_white(DevCtx* h, int p, const double* theta, int ldth, int b0, int nb) {
   // VALU from the staged tiles, r^T W r in wn_weights_kernel.  No ECORR
   // (the epoch pass would need the same split).  Dev mode 36: off (A/B)
   const bool rsep = c2 && ps.dev.n_epoch == 0 && ps.nb >= 2 && ps.dev.m <= 16 * (ps.nb - 1) &&
-                    h->kernel_mode != 36 && h->kernel_mode != 30;
+                    h->kernel_mode != 36 && h->kernel_mode != 30 &&
+                    h->kernel_mode != 38 && h->kernel_mode != 39;
   hipLaunchKernelGGL(wn_weights_kernel, dim3(nb), dim3(256), 0, h->stream, ps.dev, theta, ldth, b0, h->d_w,
                      h->d_beta, h->d_Kb, h->d_fac, rsep ? h->d_rho : nullptr);
   if (c2) {
     // (dev library A/B: mode 15 = 4 waves per sample, mode 16 = 8)
     // (30: TwoSum accumulation up to 10 blocks)
     // (35: the run remainder on the first waves, as in round 4-5a)
+    // (38 / 39: blocked accumulation up to 10 blocks, 4 / 8 waves)
     const int waves = h->kernel_mode == 15 ? 4 : h->kernel_mode == 16 ? 8 : h->kernel_mode == 30 ? 30
-                    : h->kernel_mode == 35 ? 35 : 0;
+                    : h->kernel_mode == 35 ? 35 : h->kernel_mode == 38 ? 38 : h->kernel_mode == 39 ? 39 : 0;
     int rc = launch_contract2_nb(ps.nb, waves, ps.dev, h->d_w, h->d_beta, h->d_s, h->s_stride, h->d_G, nb, h->stream,
                                  rsep ? h->d_rho : nullptr);
     if (rc) return rc;
@@ -3610,14 +3612,14 @@ int ewh_set_fixed_white(ewh_handle* H, const double* values) {
 }
 
 int ewh_set_kernel_mode(ewh_handle* H, int32_t mode) {
-  if (!H || mode < 0 || mode > 37) return set_err(EWH_E_INVALID, "bad handle / mode");
+  if (!H || mode < 0 || mode > 39) return set_err(EWH_E_INVALID, "bad handle / mode");
 #ifdef EWH_DEV
   constexpr bool dev_lib = true;   // mode 33 (the one-proposal C5 schedule with the diagonal launched apart)
 #else
   constexpr bool dev_lib = false;
 #endif
   if (mode != 0 && mode != 1 && mode != 2 && mode != 7 && mode != MODE_WIDE && mode != MODE_DD && !variant_built(mode) &&
-      !((mode == 33 || mode == MODE_WIDE_R05A || mode == 35 || mode == 36 || mode == 37) && dev_lib))
+      !((mode == 33 || mode == MODE_WIDE_R05A || (mode >= 35 && mode <= 39)) && dev_lib))
     return set_err(EWH_E_UNSUPPORTED, "kernel mode " + std::to_string(mode) +
                                           " is not built into this library (A/B variants: the dev library, make dev)");
   for (DevCtx* h : H->ctx) {
