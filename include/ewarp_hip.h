@@ -325,7 +325,8 @@ int ewh_refine_stats(ewh_handle* h, int64_t* checked, int64_t* refined);
  * the waves that also form the ECORR epoch sums), 36 = the contraction
  * without the r-separated Gram (r in the MFMA blocks, as before round 5h),
  * 37 = the wide path's ECORR epoch sums one sample per workgroup (as before
- * round 5h).  Other modes return
+ * round 5h), 38 / 39 = the varying-white-noise contraction up to 10 blocks
+ * with blocked instead of TwoSum accumulation, 4 / 8 waves.  Other modes return
  * EWH_E_UNSUPPORTED. */
 int ewh_set_kernel_mode(ewh_handle* h, int32_t mode);
 
