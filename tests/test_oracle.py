@@ -273,3 +273,27 @@ def test_device_order_extended_precision_is_closer_on_ill_conditioned_draws():
     assert z["spread"][i] > 1e-4                      # c2_small sample 1: a near-singular prior draw
     lo, hi = min(z["lnl"][i], z["lnl_dev"][i]), max(z["lnl"][i], z["lnl_dev"][i])
     assert lo - z["spread"][i] <= z["lnl_exact"][i] <= hi + z["spread"][i]
+
+
+@pytest.mark.parametrize("fixture", ["c5_prior", "c5_full"])
+def test_c5_full_size_fixtures_consistent(fixture):
+    """The full-size C5 fixtures (tests/golden/make_c5_prior.py,
+    make_c5_full.py; computed in the dev container): one value per draw and
+    reference, one theta row per draw over the model's parameters, every
+    value finite, and the device's fp64 order restated on the host within
+    strict of enterprise's order (near-truth draws) or, on prior draws, no
+    less accurate than it against the extended-precision value."""
+    import json
+    from conftest import GOLDEN, strict_tolerance
+    with open(os.path.join(GOLDEN, fixture + ".json")) as fh:
+        rec = json.load(fh)
+    X = np.array(rec["theta"])
+    assert X.shape == (len(rec["lnl"]), len(rec["param_names"])) and len(rec["lnl_dev"]) == len(X)
+    ent, dev = np.array(rec["lnl"]), np.array(rec["lnl_dev"])
+    assert np.all(np.isfinite(ent)) and np.all(np.isfinite(dev))
+    if "lnl_ext" in rec:
+        ext = np.array(rec["lnl_ext"])
+        st = strict_tolerance(ext)
+        assert np.all(np.abs(dev - ext) <= np.maximum(np.abs(ent - ext), st))
+    else:
+        assert np.all(np.abs(dev - ent) <= strict_tolerance(ent))
