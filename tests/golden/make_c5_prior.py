@@ -12,7 +12,7 @@ frequencies, fixed white noise).  Per draw:
                  precision on the error-free Gram (device_order_ref with
                  np.longdouble).
 
-Run in the dev container (CPU only, a few minutes; the extended-precision
+Run in the dev container (CPU only, ~30 min for 24 draws; the extended-precision
 dense 2,801 x 2,801 factorisation dominates):
 
     python tests/golden/make_c5_prior.py [N]
@@ -35,7 +35,7 @@ from enterprise_warp_amd import synth  # noqa: E402
 from golden.make_c5_full import synth_hash, synth_sums  # noqa: E402
 
 
-def main(n_samples=8):
+def main(n_samples=24):
     from oracle.device_order_ref import DeviceOrderPTA
     from oracle.enterprise_ref import OraclePTA
     t0 = time.time()
@@ -70,4 +70,4 @@ def main(n_samples=8):
 
 
 if __name__ == "__main__":
-    main(int(sys.argv[1]) if len(sys.argv) > 1 else 8)
+    main(int(sys.argv[1]) if len(sys.argv) > 1 else 24)

@@ -215,7 +215,7 @@ def test_c5_full_size_vs_oracle(require_gpu, c5_full):
 
 
 def test_c5_bench_workload_prior_draws(require_gpu, c5_full):
-    """The C5 bench's own workload: the first 12 of its 512 prior draws
+    """The C5 bench's own workload: the first 24 of its 512 prior draws
     (BASELINE config 5 at full size), against enterprise's order (dense
     13,200^2 cho_factor) and the near-exact value (the Woodbury form in
     extended precision on the error-free Gram), both computed in the dev
